@@ -1,0 +1,325 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (needs /root/reference; never on the GPU box):
+    python tests/golden/make_golden.py
+
+How the reference is imported: `/root/reference` is put on sys.path and
+`tests/golden/_shim` supplies an identity `numba.jit` (numba is not installed in
+this image: an ordinary ModuleNotFoundError at src/envs/utils.py:8).  For integer
+edge weights `calculate_cut_changes` (src/envs/utils.py:97-102) is integer-valued,
+so jitting cannot change any result.  The pretrained `.pth` state_dicts are read
+with `torch.load(..., weights_only=True)`.  Graph pickles under `_graphs/` are NOT
+loaded (no unpickling of reference files): graphs come from oracle/graphs.py.
+
+Every fixture is data (inputs + the reference's outputs) -- no reference source.
+"""
+import hashlib
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(HERE, "_shim"))
+
+import src.envs.core as ising_env                       # noqa: E402
+from src.envs.utils import (SingleGraphGenerator, RewardSignal, ExtraAction,   # noqa: E402
+                            OptimisationTarget, SpinBasis, DEFAULT_OBSERVABLES, Observable)
+from src.networks.mpnn import MPNN                      # noqa: E402
+from src.agents.dqn.dqn import DQN                      # noqa: E402
+from oracle import graphs                               # noqa: E402
+
+
+def env_args(mode, n, basis="SIGNED"):
+    """experiments/train_eco.py:40-50,255-264 (eco) and :311-315 (s2v)."""
+    a = {'observables': DEFAULT_OBSERVABLES,
+         'reward_signal': RewardSignal.BLS,
+         'extra_action': ExtraAction.NONE,
+         'optimisation_target': OptimisationTarget.CUT,
+         'spin_basis': SpinBasis.SIGNED if basis == "SIGNED" else SpinBasis.BINARY,
+         'norm_rewards': True,
+         'memory_length': None,
+         'horizon_length': None,
+         'stag_punishment': None,
+         'basin_reward': 1. / n,
+         'reversible_spins': True}
+    if mode == "s2v":
+        a.update(observables=[Observable.SPIN_STATE], reversible_spins=False,
+                 basin_reward=None, reward_signal=RewardSignal.DENSE)
+    if mode == "pretrained":          # experiments/pretrained_agent/test_eco.py:57-67
+        a.update(basin_reward=None, spin_basis=SpinBasis.BINARY)
+    return a
+
+
+def digest(a):
+    return np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest()[:8], dtype=np.uint64)[0]
+
+
+def run_episode(J, T, mode, spins, actions, basis="SIGNED", full_steps=None):
+    """Drive the reference env; return per-step records."""
+    n = J.shape[0]
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), T, **env_args(mode, n, basis))
+    n_obs = len(env.observables)
+    obs = env.reset(spins=spins)
+    rec = dict(obs=[obs[:n_obs].copy()], rew=[], done=[], score=[env.score], nscore=[env.normalized_score],
+               best_score=[env.best_score], best_nscore=[env.best_score_normalized],
+               best_solution=[env.best_solution], mlr=env.scorer._max_local_reward,
+               qn=env.scorer._solution_quality_normalizer, lb=env.scorer._lower_bound)
+    for a in actions:
+        obs, rew, done, _ = env.step(int(a))
+        rec["obs"].append(obs[:n_obs].copy())
+        rec["rew"].append(float(rew))
+        rec["done"].append(bool(done))
+        rec["score"].append(env.score)
+        rec["nscore"].append(env.normalized_score)
+        rec["best_score"].append(env.best_score)
+        rec["best_nscore"].append(env.best_score_normalized)
+        rec["best_solution"].append(env.best_solution)
+        if done:
+            break
+    # step past the end must raise NotImplementedError (spinsystem.py:365-367)
+    raised = False
+    if rec["done"] and rec["done"][-1] and env.current_step == env.max_steps:
+        try:
+            env.step(0)
+        except NotImplementedError:
+            raised = True
+    rec["raised_past_end"] = raised
+    return rec
+
+
+def pack_env_cases(cases, full=True, full_steps=()):
+    out = {}
+    for ci, c in enumerate(cases):
+        p = f"c{ci}_"
+        rec = c["rec"]
+        out[p + "J"] = c["J"].astype(np.int8)
+        out[p + "T"] = np.int64(c["T"])
+        out[p + "mode"] = np.array(c["mode"])
+        out[p + "basis"] = np.array(c["basis"])
+        out[p + "spins"] = np.asarray(c["spins"], dtype=np.int8)
+        out[p + "actions"] = np.asarray(c["actions"], dtype=np.int32)
+        obs = np.stack(rec["obs"])
+        if full:
+            out[p + "obs"] = obs
+        else:
+            out[p + "obs_digest"] = np.array([digest(o) for o in obs], dtype=np.uint64)
+            steps = [s for s in full_steps if s < len(obs)]
+            out[p + "obs_steps"] = np.array(steps, dtype=np.int64)
+            out[p + "obs_at"] = obs[steps]
+        for k in ("rew", "score", "nscore", "best_score", "best_nscore", "best_solution"):
+            out[p + k] = np.asarray(rec[k], dtype=np.float64)
+        out[p + "done"] = np.asarray(rec["done"], dtype=bool)
+        out[p + "mlr"] = np.float64(rec["mlr"])
+        out[p + "qn"] = np.float64(rec["qn"])
+        out[p + "lb"] = np.float64(rec["lb"])
+        out[p + "raised_past_end"] = np.bool_(rec["raised_past_end"])
+    out["n_cases"] = np.int64(len(cases))
+    return out
+
+
+def make_env_er20():
+    rng = np.random.default_rng(20)
+    cases = []
+    for gi in range(8):
+        n = 20
+        if gi == 6:
+            J = graphs.negative_mlr_graph(n, rng)            # mlr <= 0 trap
+        elif gi == 7:
+            J = graphs.er_graph(n, 0.15, rng, "uniform")     # EdgeType.UNIFORM
+        else:
+            J = graphs.er_graph(n, 0.15, rng)                # isolated vertices common at p=.15
+        T = 2 * n
+        mode = "s2v" if gi == 5 else "eco"
+        basis = "BINARY" if gi == 4 else "SIGNED"
+        if mode == "s2v":
+            spins = -np.ones(n, dtype=np.int64)
+            actions = rng.permutation(n)                      # irreversible: each spin once
+            T = n
+        else:
+            spins = 2 * rng.integers(0, 2, n) - 1
+            actions = rng.integers(0, n, T)
+        if gi == 3:
+            # revisit pattern: flip back and forth to exercise the visited-set quirk
+            actions = np.array([int(a) for a in rng.integers(0, n, T // 2) for _ in (0, 1)])
+        sp = (1 - spins) // 2 if basis == "BINARY" else spins
+        rec = run_episode(J, T, mode, sp, actions, basis)
+        cases.append(dict(J=J, T=T, mode=mode, basis=basis, spins=sp, actions=actions, rec=rec))
+    np.savez_compressed(os.path.join(HERE, "env_er20.npz"), **pack_env_cases(cases))
+
+
+def make_env_large():
+    rng = np.random.default_rng(200)
+    cases = []
+    for kind, n, extra in (("ER", 200, 0.15), ("ER", 200, 0.15), ("BA", 500, 4)):
+        J = graphs.er_graph(n, extra, rng) if kind == "ER" else graphs.ba_graph(n, extra, rng)
+        T = 2 * n
+        spins = 2 * rng.integers(0, 2, n) - 1
+        actions = rng.integers(0, n, T)
+        rec = run_episode(J, T, "eco", spins, actions)
+        cases.append(dict(J=J, T=T, mode="eco", basis="SIGNED", spins=spins, actions=actions, rec=rec))
+    np.savez_compressed(os.path.join(HERE, "env_large.npz"),
+                        **pack_env_cases(cases, full=False, full_steps=(0, 1, 2, 3, 5, 100, 200, 399, 400, 999, 1000)))
+
+
+def obs_after_random_steps(J, T, n_steps, rng, basis="SIGNED", mode="eco"):
+    n = J.shape[0]
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), T, **env_args(mode, n, basis))
+    spins = 2 * rng.integers(0, 2, n) - 1
+    obs = env.reset(spins=(1 - spins) // 2 if basis == "BINARY" else spins)
+    for a in rng.integers(0, n, n_steps):
+        obs, _, _, _ = env.step(int(a))
+    return obs
+
+
+def state_dict_np(net):
+    return {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}
+
+
+def make_mpnn():
+    rng = np.random.default_rng(7)
+    out = {}
+    # (i) pretrained ECO ER-200 weights (MIT, experiments/pretrained_agent/networks/eco)
+    sd = torch.load(os.path.join(REF, "experiments/pretrained_agent/networks/eco/network_best_ER_200spin.pth"),
+                    map_location="cpu", weights_only=True)
+    net = MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)
+    net.load_state_dict(sd)
+    net.eval()
+    for k, v in state_dict_np(net).items():
+        out["er200/" + k] = v
+    Js = [graphs.er_graph(200, 0.15, rng) for _ in range(2)]
+    obs = [obs_after_random_steps(J, 400, 37, rng) for J in Js]
+    with torch.no_grad():
+        q_b1 = [net(torch.FloatTensor(o.copy())).numpy() for o in obs]
+        q_b2 = net(torch.FloatTensor(np.array(obs))).numpy()
+    out["er200/obs"] = np.array(obs)
+    out["er200/q_b1"] = np.array(q_b1)
+    out["er200/q_b2"] = q_b2
+    # (iii) BINARY-basis observation for the same net (pretrained script's env args)
+    ob = obs_after_random_steps(Js[0], 400, 11, rng, basis="BINARY", mode="pretrained")
+    with torch.no_grad():
+        out["er200/obs_binary"] = ob
+        out["er200/q_binary"] = net(torch.FloatTensor(ob.copy())).numpy()
+    # (ii) ER-20, seeded normal(0, 0.01) init (dqn.py:199-205), batch of 8 incl. isolated vertices
+    torch.manual_seed(1234)
+    net20 = MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)
+    with torch.no_grad():
+        for m in net20.modules():
+            if type(m) == torch.nn.Linear:
+                m.weight.normal_(0, 0.01)
+    for k, v in state_dict_np(net20).items():
+        out["er20/" + k] = v
+    Js20 = [graphs.er_graph(20, 0.15, rng) for _ in range(8)]
+    obs20 = np.array([obs_after_random_steps(J, 40, 9, rng) for J in Js20])
+    with torch.no_grad():
+        out["er20/q_b8"] = net20(torch.FloatTensor(obs20)).numpy()
+        out["er20/q_b1"] = np.array([net20(torch.FloatTensor(o.copy())).numpy() for o in obs20])
+    out["er20/obs"] = obs20
+    # in-place transpose quirk (mpnn.py:44): a float32 3-D input is mutated to [B, N, 7+N]
+    t = torch.FloatTensor(obs20.copy())
+    with torch.no_grad():
+        net20(t)
+    out["er20/input_after_forward"] = t.numpy()
+    np.savez_compressed(os.path.join(HERE, "mpnn_fwd.npz"), **out)
+
+
+def make_dqn_step():
+    """Three consecutive DQN.train_step calls (dqn.py:403-451) on ER-20 transitions."""
+    rng = np.random.default_rng(99)
+    n, M = 20, 16
+    J = graphs.er_graph(n, 0.15, rng)
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), 2 * n, **env_args("eco", n))
+    net_fn = lambda: MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)  # noqa: E731
+    agent = DQN([env], net_fn, init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
+                replay_start_size=10, replay_buffer_size=100, gamma=0.95, update_target_frequency=1000,
+                update_learning_rate=False, initial_learning_rate=1e-4, peak_learning_rate=1e-4,
+                final_learning_rate=1e-4, update_frequency=32, minibatch_size=M, max_grad_norm=None,
+                weight_decay=0, update_exploration=True, initial_exploration_rate=1,
+                final_exploration_rate=0.05, final_exploration_step=150000, adam_epsilon=1e-8,
+                logging=False, loss="mse", save_network_frequency=10**9, network_save_path="/tmp/n.pth",
+                evaluate=False, test_envs=None, test_episodes=1, test_frequency=10**9,
+                test_save_path="/tmp/ts.pkl", seed=5)
+    # perturb the target net so double-DQN's argmax(online) != argmax(target) matters
+    with torch.no_grad():
+        for p in agent.target_network.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    out = {}
+    for k, v in state_dict_np(agent.network).items():
+        out["w0/" + k] = v
+    for k, v in state_dict_np(agent.target_network).items():
+        out["target/" + k] = v
+    steps = 3
+    for s in range(steps):
+        sts, acts, rews, nxt, dns = [], [], [], [], []
+        for _ in range(M):
+            Jg = graphs.er_graph(n, 0.15, rng)
+            e = ising_env.make("SpinSystem", SingleGraphGenerator(Jg), 2 * n, **env_args("eco", n))
+            o = e.reset(spins=2 * rng.integers(0, 2, n) - 1)
+            for a in rng.integers(0, n, int(rng.integers(0, 2 * n - 1))):
+                o, _, _, _ = e.step(int(a))
+            a = int(rng.integers(0, n))
+            o2, r, d, _ = e.step(a)
+            sts.append(o); acts.append([a]); rews.append([r]); nxt.append(o2); dns.append([float(d)])
+        tr = [torch.as_tensor(np.array(sts)), torch.as_tensor(np.array(acts), dtype=torch.long),
+              torch.as_tensor(np.array(rews), dtype=torch.float), torch.as_tensor(np.array(nxt)),
+              torch.as_tensor(np.array(dns), dtype=torch.float)]
+        out[f"s{s}/states"] = np.array(sts)
+        out[f"s{s}/actions"] = np.array(acts)
+        out[f"s{s}/rewards"] = np.array(rews, dtype=np.float32)
+        out[f"s{s}/states_next"] = np.array(nxt)
+        out[f"s{s}/dones"] = np.array(dns, dtype=np.float32)
+        loss = agent.train_step(tr)
+        out[f"s{s}/loss"] = np.float64(loss)
+        for k, v in state_dict_np(agent.network).items():
+            out[f"s{s}/w/" + k] = v
+    out["steps"] = np.int64(steps)
+    np.savez_compressed(os.path.join(HERE, "dqn_step.npz"), **out)
+
+
+def make_greedy_rollout():
+    """Pretrained-net greedy rollout (dqn.py:490-512 predict) on one ER-200 graph:
+    actions plus the top-1/top-2 Q margin per step (argmax-tie robustness)."""
+    rng = np.random.default_rng(4242)
+    n = 200
+    J = graphs.er_graph(n, 0.15, rng)
+    sd = torch.load(os.path.join(REF, "experiments/pretrained_agent/networks/eco/network_best_ER_200spin.pth"),
+                    map_location="cpu", weights_only=True)
+    net = MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)
+    net.load_state_dict(sd)
+    net.eval()
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), 2 * n, **env_args("eco", n))
+    spins = 2 * rng.integers(0, 2, n) - 1
+    obs = env.reset(spins=spins)
+    acts, margins, rews = [], [], []
+    done = False
+    with torch.no_grad():
+        while not done:
+            q = net(torch.FloatTensor(obs.copy()))
+            top = torch.topk(q, 2).values
+            a = int(q.argmax().item())
+            acts.append(a)
+            margins.append(float(top[0] - top[1]))
+            obs, r, done, _ = env.step(a)
+            rews.append(float(r))
+    np.savez_compressed(os.path.join(HERE, "greedy_er200.npz"), J=J.astype(np.int8), spins=spins.astype(np.int8),
+                        actions=np.array(acts, np.int32), margins=np.array(margins), rewards=np.array(rews),
+                        best_solution=np.float64(env.best_solution), best_score=np.float64(env.best_score))
+
+
+if __name__ == "__main__":
+    random.seed(0)
+    np.random.seed(0)
+    make_env_er20()
+    make_env_large()
+    make_mpnn()
+    make_dqn_step()
+    make_greedy_rollout()
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
