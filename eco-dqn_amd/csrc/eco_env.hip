@@ -1,0 +1,567 @@
+// Batched MaxCut SpinSystem on gfx950: graph preparation, reset, step, read-out.
+//
+// One 64-lane wave owns one episode; lane l owns vertices l, l+64, ... (VPT per
+// lane), so every per-vertex reduction of the reference step (count of positive
+// gains, all(g<=0), Hamming distance to best, the visited-state bitset) is a
+// ballot/popcount and the episode scalars live in SGPRs.  The local field
+// h = J.s is kept resident and updated by ONE CSR row per flip
+// (h_j -= 2 w_aj s_a), so a step touches deg(a) edges instead of the reference's
+// four dense J@s matvecs and two dense calculate_cut quadratic forms
+// (spinsystem.py:393-416, 516-519).  All scores are exact integers in f64, and the
+// f64 observation values are produced by the same IEEE operations as the
+// reference, so rewards/observations match it bit for bit.
+#include "eco_common.h"
+
+namespace eco {
+
+// ------------------------------------------------------------------ graphs ----
+// score_solver.py:347-375 (normalisers) and mpnn.py:34-38 (degree norm).
+__global__ __launch_bounds__(256) void graphs_prepare_kernel(eco_graph_set gs) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= gs.n_graphs) return;
+  const int N = gs.n_spins;
+  const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
+  const uint32_t* ed = gs.edges + gs.edge_base[g];
+  long long pos = 0, neg = 0, sum = 0;
+  int mdeg = 1;
+  int best = INT_MIN;
+  int has = 0;
+  for (int v = lane; v < N; v += 64) {
+    int rs = 0, d = 0;
+    for (int e = rp[v]; e < rp[v + 1]; ++e) {
+      const int w = edge_w(ed[e]);
+      rs += w;
+      d += (w != 0);
+      if (w > 0) pos += w; else neg += w;
+    }
+    sum += rs;
+    gs.deg[(size_t)g * N + v] = d;
+    mdeg = max(mdeg, max(d, 1));
+    // g(s=-1)_v = (-1) * (J.(-1))_v = row sum; mlr = max over NONZERO entries
+    if (rs != 0) { has = 1; best = max(best, rs); }
+  }
+  pos = wave_sum_ll(pos);
+  neg = wave_sum_ll(neg);
+  sum = wave_sum_ll(sum);
+  mdeg = wave_max_i(mdeg);
+  best = wave_max_i(best);
+  has = wave_max_i(has);
+  if (lane == 0) {
+    gs.max_deg[g] = mdeg;
+    gs.valid[g] = has;
+    double* m = gs.meta + (size_t)g * 4;
+    m[0] = has ? (double)best : 1.0;
+    const double q = (double)pos / 2.0;  // np.sum(J*(J>0))/2
+    m[1] = q > 1.0 ? q : 1.0;            // max(1, .)
+    const double lb = (double)neg / 2.0;
+    m[2] = lb < 0.0 ? lb : 0.0;          // min(0, .)
+    m[3] = (double)sum;
+  }
+}
+
+// ------------------------------------------------------------- env kernels ----
+struct EnvArgs {
+  eco_env_config cfg;
+  eco_graph_set gs;
+  EnvLayout L;
+  uint8_t* state;
+  int B;
+  const int32_t* graph_ids;
+  const int8_t* spins_in;
+  const uint8_t* mask;
+  uint64_t seed;
+  const int32_t* actions;
+  double* rewards;
+  uint8_t* dones;
+  float* obs_x;
+  double* obs_f64;
+  int32_t* err;  // device error word (first error wins)
+};
+
+__device__ __forceinline__ EpScal* scal_ptr(const EnvArgs& a) { return (EpScal*)(a.state + a.L.off_scal); }
+__device__ __forceinline__ const double* tab_ptr(const EnvArgs& a) { return (const double*)(a.state + a.L.off_tab + 256); }
+
+// time table: tab[k] = running f64 sum of k additions of 1/T (spinsystem.py:493, :506)
+__global__ void build_time_table_kernel(uint8_t* state, size_t off_tab, int T) {
+  int* hdr = (int*)(state + off_tab);
+  if (*hdr == T) return;
+  double* tab = (double*)(state + off_tab + 256);
+  double v = 0.0;
+  const double inc = 1.0 / (double)T;
+  tab[0] = 0.0;
+  for (int k = 1; k <= T; ++k) { v += inc; tab[k] = v; }
+  *hdr = T;
+}
+
+// One observable row value, float64, exactly as spinsystem.py:303-328 / :486-535.
+struct ObsCtx {
+  double mlr, dist_best, hamming, nqi, term, ep_time;
+  int basis;
+};
+__device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int g, int tsfk, const double* tab) {
+  switch (id) {
+    case ECO_OBS_SPIN_STATE: return c.basis == ECO_BASIS_BINARY ? (double)(1 - s) / 2.0 : (double)s;
+    case ECO_OBS_IMMEDIATE_QUALITY_CHANGE: return (double)g / c.mlr;
+    case ECO_OBS_TIME_SINCE_FLIP: return tab[tsfk];
+    case ECO_OBS_EPISODE_TIME: return c.ep_time;
+    case ECO_OBS_TERMINATION_IMMANENCY: return c.term;
+    case ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS: return c.nqi;
+    case ECO_OBS_DISTANCE_FROM_BEST_SOLUTION: return c.dist_best;
+    case ECO_OBS_DISTANCE_FROM_BEST_STATE: return c.hamming;
+    case ECO_OBS_IMMEDIATE_VALIDITY_CHANGE: return 1.0;  // MaxCut: every flip valid
+    case ECO_OBS_VALIDITY_BIT: return 1.0;
+    default: return 0.0;  // validity differences are identically 0 for MaxCut
+  }
+}
+
+template <int VPT>
+__device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, const int (&s)[VPT], const int (&g)[VPT],
+                                          const int (&tsf)[VPT], const ObsCtx& c) {
+  const int N = a.cfg.n_spins;
+  const int nobs = a.cfg.n_obs;
+  const double* tab = tab_ptr(a);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v >= N) continue;
+    float xf[ECO_MAX_OBS];
+#pragma unroll
+    for (int i = 0; i < ECO_MAX_OBS; ++i) {
+      double val = 0.0;
+      if (i < nobs) {
+        val = obs_value(a.cfg.obs_ids[i], c, s[k], g[k], tsf[k], tab);
+        if (a.obs_f64) a.obs_f64[((size_t)e * nobs + i) * N + v] = val;
+      }
+      xf[i] = (float)val;
+    }
+    if (a.obs_x) {
+      float4* dst = (float4*)(a.obs_x + ((size_t)e * N + v) * ECO_MAX_OBS);
+      dst[0] = make_float4(xf[0], xf[1], xf[2], xf[3]);
+      dst[1] = make_float4(xf[4], xf[5], xf[6], xf[7]);
+    }
+  }
+}
+
+// SpinSystemBase.reset (spinsystem.py:183-259) + _reset_state (:283-330)
+template <int VPT>
+__global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
+  extern __shared__ int8_t s_lds[];  // [4 waves][N] spins staged for the J.s matvec
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int e = uniform_i(blockIdx.x * 4 + wv);
+  if (e >= a.B) return;
+  if (a.mask && !a.mask[e]) return;
+  const int N = a.cfg.n_spins;
+  const EnvLayout& L = a.L;
+  int8_t* my_s = s_lds + wv * N;
+  const int gid = uniform_i(a.graph_ids[e]);
+  if (gid < 0 || gid >= a.gs.n_graphs || !a.gs.valid[gid]) {
+    if (lane == 0) atomicCAS(a.err, 0, ECO_ERR_GRAPH);
+    return;
+  }
+  const double* meta = a.gs.meta + (size_t)gid * 4;
+  const double mlr = meta[0], qn = meta[1], lb = meta[2];
+  const long long sumJ = (long long)meta[3];
+  int s[VPT], h[VPT], g[VPT], tsf[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    int sv = 0;
+    if (v < N) {
+      if (a.spins_in) {
+        sv = a.spins_in[(size_t)e * N + v];
+        if (sv != 1 && sv != -1) { atomicCAS(a.err, 0, ECO_ERR_BASIS); sv = -1; }
+      } else if (a.cfg.reversible_spins) {
+        sv = (int)(rng3(a.seed, (uint64_t)e, (uint64_t)v) >> 63) * 2 - 1;  // 2*randint(2)-1
+      } else {
+        sv = -1;  // irreversible: all -1 (spinsystem.py:295-297)
+      }
+      my_s[v] = (int8_t)sv;
+    }
+    s[k] = sv;
+    tsf[k] = 0;
+  }
+  // each wave reads back only its own LDS slice: a wave-scope fence suffices
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
+  const uint32_t* ed = a.gs.edges + a.gs.edge_base[gid];
+  long long sg = 0;
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    int hv = 0;
+    if (v < N) {
+      for (int q = rp[v]; q < rp[v + 1]; ++q) {
+        const uint32_t x = ed[q];
+        hv += edge_w(x) * (int)my_s[edge_col(x)];
+      }
+    }
+    h[k] = hv;
+    g[k] = s[k] * hv;  // calculate_cut_changes: s * (J @ s)
+    sg += g[k];
+    cnt += (g[k] > 0);
+  }
+  sg = wave_sum_ll(sg);
+  cnt = wave_sum_i(cnt);
+  // calculate_cut = 1/4 sum J (1 - s s^T) = (sum J - s.Js)/4, exact integer for integer weights
+  const double cut = (double)((sumJ - sg) / 4);
+  const double lbabs = lb < 0.0 ? -lb : lb;
+  const double score = cut + lbabs;        // MaximizationProblem.get_score (score_solver.py:182-188)
+  const double nscore = score / qn;        // get_normalized_score (:190-194)
+  int8_t* gsp = (int8_t*)(a.state + L.off_spins) + (size_t)e * N;
+  int32_t* gh = (int32_t*)(a.state + L.off_field) + (size_t)e * N;
+  int16_t* gt = (int16_t*)(a.state + L.off_tsf) + (size_t)e * N;
+  int8_t* gb = (int8_t*)(a.state + L.off_best) + (size_t)e * N;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) { gsp[v] = (int8_t)s[k]; gh[v] = h[k]; gt[v] = 0; gb[v] = (int8_t)s[k]; }
+  }
+  uint32_t* vidx = (uint32_t*)(a.state + L.off_vidx) + (size_t)e * L.cap;
+  for (int i = lane; i < L.cap; i += 64) vidx[i] = 0u;
+  if (lane == 0) {
+    EpScal* sc = scal_ptr(a) + e;
+    sc->score = score; sc->nscore = nscore;
+    sc->best_score = score; sc->best_nscore = nscore; sc->best_solution = cut;
+    sc->mlr = mlr; sc->qn = qn; sc->lbabs = lbabs;
+    sc->hash = 0ull; sc->t = 0; sc->hamming = 0; sc->graph = gid; sc->done = 0; sc->early = 0;
+    sc->visit_count = 0;
+  }
+  ObsCtx c;
+  c.mlr = mlr; c.dist_best = 0.0; c.hamming = 0.0; c.nqi = (double)cnt / (double)N;
+  c.term = 0.0; c.ep_time = 0.0; c.basis = a.cfg.spin_basis;
+  write_obs<VPT>(a, e, lane, s, g, tsf, c);
+}
+
+// SpinSystemBase.step (spinsystem.py:355-559), ExtraAction.NONE, memory_length None.
+template <int VPT>
+__global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int e = uniform_i(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (e >= a.B) return;
+  const int N = a.cfg.n_spins;
+  const int T = a.cfg.max_steps;
+  const EnvLayout& L = a.L;
+  EpScal* sc = scal_ptr(a) + e;
+  if (sc->done) {  // auto-masked
+    if (lane == 0) { a.rewards[e] = 0.0; a.dones[e] = 1; }
+    return;
+  }
+  const int act = uniform_i(a.actions[e]);
+  if (act < 0 || act >= N) {
+    if (lane == 0) { atomicCAS(a.err, 0, ECO_ERR_ARG); a.rewards[e] = 0.0; a.dones[e] = 0; }
+    return;
+  }
+  const int t = sc->t + 1;  // :362
+  int8_t* gsp = (int8_t*)(a.state + L.off_spins) + (size_t)e * N;
+  int32_t* gh = (int32_t*)(a.state + L.off_field) + (size_t)e * N;
+  int16_t* gt = (int16_t*)(a.state + L.off_tsf) + (size_t)e * N;
+  int8_t* gb = (int8_t*)(a.state + L.off_best) + (size_t)e * N;
+  const int sa_old = gsp[act];
+  const int delta_i = sa_old * gh[act];  // get_score_mask(state)[action] (:393)
+  const double qn = sc->qn, mlr = sc->mlr;
+  const double delta = (double)delta_i;
+  const double delta_n = delta / qn;     // get_normalized_score_mask(state)[action] (:394)
+  const double score = sc->score + delta;           // :399
+  const double nscore = sc->nscore + delta_n;       // :400 (accumulated)
+  int s[VPT], h[VPT], tsf[VPT], bs[VPT], g[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) { s[k] = gsp[v]; h[k] = gh[v]; tsf[k] = gt[v]; bs[k] = gb[v]; }
+    else { s[k] = 0; h[k] = 0; tsf[k] = 0; bs[k] = 0; }
+  }
+  // incremental local field: h_j -= 2 w_aj s_a(old) over the CSR row of `act`
+  {
+    const int gid = sc->graph;
+    const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
+    const uint32_t* ed = a.gs.edges + a.gs.edge_base[gid];
+    const int q1 = rp[act + 1];
+    for (int q = rp[act]; q < q1; ++q) {
+      const uint32_t x = ed[q];
+      const int j = edge_col(x);
+      const int d = -2 * edge_w(x) * sa_old;
+      if ((j & 63) == lane) {
+        const int kk = j >> 6;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) h[k] += (k == kk) ? d : 0;
+      }
+    }
+  }
+  // flip + time-since-flip counters (:397, :492-497)
+  int cnt = 0;
+  uint64_t words[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v == act) { s[k] = -s[k]; tsf[k] = 0; }
+    else if (v < N) { tsf[k] = tsf[k] + 1; }
+    g[k] = s[k] * h[k];  // immediate quality / score changes (:414, :416)
+    cnt += __popcll(__ballot(g[k] > 0));
+    words[k] = __ballot(s[k] > 0);
+  }
+  const int negs = [&] { int c = 0;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) c += __popcll(__ballot(s[k] < 0)); return c; }();
+  // HistoryBuffer.update (utils.py:444-464): is the flipped set (== spin configuration) new?
+  bool isnew = true;
+  const bool need_hist = a.cfg.has_basin_reward || a.cfg.has_stag_punishment;
+  if (need_hist) {
+    const uint64_t hash = sc->hash ^ zobrist(act);
+    const int cap = L.cap;
+    const int W = L.words;
+    uint32_t* vidx = (uint32_t*)(a.state + L.off_vidx) + (size_t)e * cap;
+    uint64_t* vh = (uint64_t*)(a.state + L.off_vhash) + (size_t)e * cap;
+    uint64_t* vst = (uint64_t*)(a.state + L.off_vstates) + (size_t)e * (T + 1) * W;
+    int slot = (int)(hash & (uint64_t)(cap - 1));
+    for (;;) {
+      const uint32_t id = vidx[slot];
+      if (id == 0u) break;
+      if (vh[slot] == hash) {
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) same = same && (vst[(size_t)(id - 1) * W + k] == words[k]);
+        if (same) { isnew = false; break; }
+      }
+      slot = (slot + 1) & (cap - 1);
+    }
+    if (lane == 0) {
+      sc->hash = hash;
+      if (isnew) {
+        const int n = sc->visit_count;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) vst[(size_t)n * W + k] = words[k];
+        vh[slot] = hash;
+        vidx[slot] = (uint32_t)(n + 1);
+        sc->visit_count = n + 1;
+      }
+    }
+  }
+  // reward (:418-457)
+  double best_score = sc->best_score, best_nscore = sc->best_nscore;
+  double rew = 0.0;
+  int early = sc->early + 1;
+  const bool improved = score > best_score;
+  if (improved) {
+    early = 0;
+    if (a.cfg.reward_signal == ECO_REWARD_BLS)
+      rew = a.cfg.norm_rewards ? nscore - best_nscore : score - best_score;
+  }
+  if (a.cfg.reward_signal == ECO_REWARD_DENSE) rew = a.cfg.norm_rewards ? delta_n : delta;
+  if (a.cfg.has_stag_punishment && !isnew) rew -= a.cfg.stag_punishment;
+  if (a.cfg.has_basin_reward && cnt == 0 && isnew) rew += a.cfg.basin_reward;
+  // best tracking (:459-477)
+  double best_solution = sc->best_solution;
+  if (improved) {
+    best_score = score;
+    best_nscore = nscore;
+    best_solution = score - sc->lbabs;  // calculate_cut(best_spins), exact for integer weights
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) bs[k] = s[k];
+  }
+  int ham = 0;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) ham += __popcll(__ballot(bs[k] != s[k]));
+  // termination (:541-556)
+  bool done = (t == T);
+  if (a.cfg.stopping == ECO_STOP_EARLY && early == 15) done = true;
+  if (a.cfg.stopping == ECO_STOP_QUARTER && t == T / 4) done = true;
+  if (!a.cfg.reversible_spins && negs == 0) done = true;
+  // write back
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) {
+      gsp[v] = (int8_t)s[k];
+      gh[v] = h[k];
+      gt[v] = (int16_t)tsf[k];
+      if (improved) gb[v] = (int8_t)bs[k];
+    }
+  }
+  if (lane == 0) {
+    sc->score = score; sc->nscore = nscore;
+    sc->best_score = best_score; sc->best_nscore = best_nscore; sc->best_solution = best_solution;
+    sc->t = t; sc->hamming = ham; sc->done = done ? 1 : 0; sc->early = early;
+    a.rewards[e] = rew;
+    a.dones[e] = done ? 1 : 0;
+  }
+  ObsCtx c;
+  c.mlr = mlr;
+  const double dsc = score - best_score;
+  c.dist_best = (dsc < 0.0 ? -dsc : dsc) / mlr;                       // :516-519
+  c.hamming = (double)ham;                                            // :526-527
+  c.nqi = (double)cnt / (double)N;                                    // :513-514
+  const double x = (double)(t - T) / (double)a.cfg.horizon_length + 1.0;
+  c.term = x > 0.0 ? x : 0.0;                                         // :509-511
+  c.ep_time = tab_ptr(a)[t];                                          // :506
+  c.basis = a.cfg.spin_basis;
+  write_obs<VPT>(a, e, lane, s, g, tsf, c);
+}
+
+// read-out of episode scalars / spins
+__global__ void env_read_kernel(EnvArgs a, double* scalars, int8_t* spins, int8_t* best) {
+  const int e = blockIdx.x;
+  if (e >= a.B) return;
+  const int N = a.cfg.n_spins;
+  const EpScal* sc = scal_ptr(a) + e;
+  if (threadIdx.x == 0 && scalars) {
+    double* o = scalars + (size_t)e * 8;
+    o[0] = sc->t; o[1] = sc->score; o[2] = sc->nscore; o[3] = sc->best_score;
+    o[4] = sc->best_nscore; o[5] = sc->best_solution; o[6] = sc->hamming; o[7] = sc->done;
+  }
+  const int8_t* gsp = (const int8_t*)(a.state + a.L.off_spins) + (size_t)e * N;
+  const int8_t* gb = (const int8_t*)(a.state + a.L.off_best) + (size_t)e * N;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) {
+    if (spins) spins[(size_t)e * N + v] = gsp[v];
+    if (best) best[(size_t)e * N + v] = gb[v];
+  }
+}
+
+// ------------------------------------------------------------------ host ----
+static int validate_cfg(const eco_env_config* c) {
+  if (!c) return fail(ECO_ERR_ARG, "null env config");
+  if (c->n_spins < 1 || c->n_spins > ECO_MAX_SPINS)
+    return fail(ECO_ERR_ARG, "n_spins out of range [1, " + std::to_string(ECO_MAX_SPINS) + "]");
+  if (c->max_steps < 1 || c->max_steps > 32767) return fail(ECO_ERR_ARG, "max_steps out of range [1, 32767]");
+  if (c->n_obs < 1 || c->n_obs > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs out of range [1, 8]");
+  if (c->obs_ids[0] != ECO_OBS_SPIN_STATE)
+    return fail(ECO_ERR_OBSERVABLE, "First observable must be Observation.SPIN_STATE.");
+  for (int i = 0; i < c->n_obs; ++i)
+    if (c->obs_ids[i] < 1 || c->obs_ids[i] > 13) return fail(ECO_ERR_ARG, "unknown observable id");
+  if (c->spin_basis != ECO_BASIS_SIGNED && c->spin_basis != ECO_BASIS_BINARY)
+    return fail(ECO_ERR_BASIS, "Unrecognised SpinBasis");
+  if (c->horizon_length < 1) return fail(ECO_ERR_ARG, "horizon_length must be >= 1");
+  return ECO_OK;
+}
+
+static int validate_gs(const eco_graph_set* gs, int N) {
+  if (!gs || !gs->row_ptr || !gs->edge_base || !gs->edges || !gs->deg || !gs->max_deg || !gs->meta || !gs->valid)
+    return fail(ECO_ERR_ARG, "incomplete graph set");
+  if (gs->n_spins != N) return fail(ECO_ERR_ARG, "graph set n_spins does not match the env");
+  if (gs->n_graphs < 1) return fail(ECO_ERR_ARG, "empty graph set");
+  return ECO_OK;
+}
+
+static int32_t* err_word() {
+  static int32_t* w = nullptr;  // one device word per process (read back after each call)
+  if (!w) {
+    if (hipMalloc(&w, sizeof(int32_t)) != hipSuccess) return nullptr;
+    (void)hipMemset(w, 0, sizeof(int32_t));
+  }
+  return w;
+}
+
+static int check_err_word(int32_t* w, hipStream_t st) {
+  int32_t h = 0;
+  if (hipMemcpyAsync(&h, w, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(ECO_ERR_HIP, "error-word readback failed");
+  if (h != 0) {
+    (void)hipMemsetAsync(w, 0, sizeof(int32_t), st);
+    (void)hipStreamSynchronize(st);
+    switch (h) {
+      case ECO_ERR_GRAPH: return fail(h, "graph has no nonzero local reward (empty graph) or bad graph id");
+      case ECO_ERR_BASIS: return fail(h, "SpinSystem is configured for signed spins ([-1,1]).");
+      case ECO_ERR_ARG: return fail(h, "action out of range [0, n_spins)");
+      default: return fail(h, "device error");
+    }
+  }
+  return ECO_OK;
+}
+
+#define ECO_DISPATCH_VPT(N, CALL)                                   \
+  do {                                                              \
+    if ((N) <= 64) { constexpr int V = 1; CALL; }                   \
+    else if ((N) <= 128) { constexpr int V = 2; CALL; }             \
+    else if ((N) <= 256) { constexpr int V = 4; CALL; }             \
+    else if ((N) <= 512) { constexpr int V = 8; CALL; }             \
+    else if ((N) <= 1024) { constexpr int V = 16; CALL; }           \
+    else { constexpr int V = 32; CALL; }                            \
+  } while (0)
+
+}  // namespace eco
+
+using namespace eco;
+
+extern "C" int eco_graphs_prepare(eco_graph_set* gs, eco_stream_t stream) {
+  if (!gs || !gs->row_ptr || !gs->edge_base || !gs->edges || !gs->deg || !gs->max_deg || !gs->meta || !gs->valid)
+    return fail(ECO_ERR_ARG, "incomplete graph set");
+  if (gs->n_graphs < 1 || gs->n_spins < 1) return fail(ECO_ERR_ARG, "empty graph set");
+  const int blocks = (gs->n_graphs + 3) / 4;
+  graphs_prepare_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*gs);
+  return check_launch("graphs_prepare");
+}
+
+extern "C" size_t eco_env_state_bytes(const eco_env_config* cfg, int32_t batch) {
+  if (validate_cfg(cfg) != ECO_OK || batch < 1) return 0;
+  return env_layout(cfg->n_spins, cfg->max_steps, batch).total;
+}
+
+static int make_args(EnvArgs& a, const eco_env_config* cfg, const eco_graph_set* gs, void* state, int32_t batch) {
+  int rc = validate_cfg(cfg);
+  if (rc) return rc;
+  if (gs) { rc = validate_gs(gs, cfg->n_spins); if (rc) return rc; }
+  if (!state) return fail(ECO_ERR_ARG, "null state");
+  if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
+  a = EnvArgs{};
+  a.cfg = *cfg;
+  if (gs) a.gs = *gs;
+  a.L = env_layout(cfg->n_spins, cfg->max_steps, batch);
+  a.state = (uint8_t*)state;
+  a.B = batch;
+  a.err = err_word();
+  if (!a.err) return fail(ECO_ERR_HIP, "cannot allocate error word");
+  return ECO_OK;
+}
+
+extern "C" int eco_env_reset(const eco_env_config* cfg, const eco_graph_set* gs, void* state, int32_t batch,
+                             const int32_t* graph_ids, const int8_t* spins, const uint8_t* reset_mask, uint64_t seed,
+                             float* obs_x, double* obs_f64, eco_stream_t stream) {
+  EnvArgs a;
+  int rc = make_args(a, cfg, gs, state, batch);
+  if (rc) return rc;
+  if (!gs) return fail(ECO_ERR_ARG, "null graph set");
+  if (!graph_ids) return fail(ECO_ERR_ARG, "null graph_ids");
+  a.graph_ids = graph_ids; a.spins_in = spins; a.mask = reset_mask; a.seed = seed;
+  a.obs_x = obs_x; a.obs_f64 = obs_f64;
+  hipStream_t st = (hipStream_t)stream;
+  build_time_table_kernel<<<1, 1, 0, st>>>(a.state, a.L.off_tab, cfg->max_steps);
+  const int blocks = (batch + 3) / 4;
+  const size_t lds = (size_t)4 * cfg->n_spins;
+  ECO_DISPATCH_VPT(cfg->n_spins, (env_reset_kernel<V><<<blocks, 256, lds, st>>>(a)));
+  return check_launch("env_reset");
+}
+
+extern "C" int eco_check_errors(eco_stream_t stream) {
+  int32_t* w = err_word();
+  if (!w) return fail(ECO_ERR_HIP, "cannot allocate error word");
+  return check_err_word(w, (hipStream_t)stream);
+}
+
+extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, void* state, int32_t batch,
+                            const int32_t* actions, double* rewards, uint8_t* dones, float* obs_x, double* obs_f64,
+                            eco_stream_t stream) {
+  EnvArgs a;
+  int rc = make_args(a, cfg, gs, state, batch);
+  if (rc) return rc;
+  if (!gs) return fail(ECO_ERR_ARG, "null graph set");
+  if (!actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null actions/rewards/dones");
+  a.actions = actions; a.rewards = rewards; a.dones = dones; a.obs_x = obs_x; a.obs_f64 = obs_f64;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (batch + 3) / 4;
+  ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, 0, st>>>(a)));
+  return check_launch("env_step");
+}
+
+extern "C" int eco_env_read(const eco_env_config* cfg, const void* state, int32_t batch, double* scalars,
+                            int8_t* spins, int8_t* best_spins, eco_stream_t stream) {
+  EnvArgs a;
+  int rc = make_args(a, cfg, nullptr, (void*)state, batch);
+  if (rc) return rc;
+  env_read_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(a, scalars, spins, best_spins);
+  return check_launch("env_read");
+}

@@ -1,0 +1,147 @@
+"""Batched MaxCut SpinSystem: B concurrent episodes on one GPU (libecohip env kernels).
+
+The reference steps one `SpinSystemBase` at a time from a Python loop
+(dqn.py:273-327, experiments/utils.py:169-201).  `VecSpinSystem` holds B episodes
+in one device state buffer and advances all of them with one kernel launch; the
+per-episode semantics are exactly spinsystem.py:183-559 (bit-exact f64 rewards and
+observations, see tests/test_env_gpu.py).
+"""
+import ctypes
+
+import torch
+
+from .. import _lib
+from .utils import (DEFAULT_OBSERVABLES, ExtraAction, Observable, OptimisationTarget, RewardSignal,
+                    SpinBasis, Stopping)
+
+
+def make_config(n_spins, max_steps, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.DENSE,
+                extra_action=ExtraAction.PASS, optimisation_target=OptimisationTarget.ENERGY,
+                spin_basis=SpinBasis.SIGNED, norm_rewards=False, memory_length=None, horizon_length=None,
+                stag_punishment=None, basin_reward=None, reversible_spins=True, stopping=Stopping.NORMAL,
+                **_ignored):
+    """env_args (spinsystem.py:29-48 defaults) -> eco_env_config."""
+    if optimisation_target != OptimisationTarget.CUT:
+        # the reference factory has no ENERGY branch (score_solver.py:866-885); other
+        # problems are off the MaxCut hot path
+        raise NotImplementedError(f"Invalid optimization target: {optimisation_target} (eco_hip runs CUT only)")
+    if extra_action != ExtraAction.NONE:
+        raise NotImplementedError("eco_hip runs ExtraAction.NONE only (PASS shape-breaks the reference "
+                                  "score mask, spinsystem.py:141-142,393)")
+    if memory_length is not None:
+        raise NotImplementedError("finite memory_length is not on the hot path")
+    obs = list(observables)
+    assert obs[0] == Observable.SPIN_STATE, "First observable must be Observation.SPIN_STATE."
+    if len(obs) > _lib.ECO_MAX_OBS:
+        raise ValueError("at most 8 observables")
+    if spin_basis not in (SpinBasis.SIGNED, SpinBasis.BINARY):
+        raise Exception("Unrecognised SpinBasis")
+    c = _lib.EnvConfig()
+    c.n_spins = n_spins
+    c.max_steps = max_steps
+    c.n_obs = len(obs)
+    for i, o in enumerate(obs):
+        c.obs_ids[i] = o.value
+    c.reward_signal = reward_signal.value
+    c.norm_rewards = int(bool(norm_rewards))
+    c.reversible_spins = int(bool(reversible_spins))
+    c.spin_basis = spin_basis.value
+    c.stopping = stopping.value
+    c.has_basin_reward = int(basin_reward is not None)
+    c.basin_reward = float(basin_reward) if basin_reward is not None else 0.0
+    c.has_stag_punishment = int(stag_punishment is not None)
+    c.stag_punishment = float(stag_punishment) if stag_punishment is not None else 0.0
+    c.horizon_length = int(horizon_length if horizon_length is not None else max_steps)
+    return c
+
+
+class VecSpinSystem:
+    """B MaxCut episodes over graphs of a GraphStore.
+
+    reset(graph_ids, spins=None, mask=None, seed=0) and step(actions) return the
+    fp32 node features obs_x [B, N, 8] that the MPNN consumes (obs.float() of the
+    reference observation rows, dqn.py:282); pass want_f64=True to also fill
+    obs_f64 [B, n_obs, N] (the reference's float64 rows, for parity checks)."""
+
+    def __init__(self, graphs, n_envs, max_steps, want_f64=False, stream=None, **env_args):
+        self.graphs = graphs
+        self.n_envs = n_envs
+        self.n_spins = graphs.n_spins
+        self.max_steps = max_steps
+        self.env_args = env_args
+        self.cfg = make_config(graphs.n_spins, max_steps, **env_args)
+        self.n_obs = self.cfg.n_obs
+        self.reversible_spins = bool(self.cfg.reversible_spins)
+        self.spin_basis = env_args.get("spin_basis", SpinBasis.SIGNED)
+        dev = graphs.device
+        nbytes = _lib.lib.eco_env_state_bytes(ctypes.byref(self.cfg), n_envs)
+        if nbytes == 0:
+            raise ValueError(_lib.last_error())
+        self.state = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        self.obs_x = torch.zeros(n_envs, self.n_spins, _lib.ECO_MAX_OBS, dtype=torch.float32, device=dev)
+        self.obs_f64 = (torch.zeros(n_envs, self.n_obs, self.n_spins, dtype=torch.float64, device=dev)
+                        if want_f64 else None)
+        self.rewards = torch.zeros(n_envs, dtype=torch.float64, device=dev)
+        self.dones = torch.zeros(n_envs, dtype=torch.uint8, device=dev)
+        self.graph_ids = torch.zeros(n_envs, dtype=torch.int32, device=dev)
+        self.scalars = torch.zeros(n_envs, 8, dtype=torch.float64, device=dev)
+        self.stream = stream
+
+    def _s(self):
+        return _lib.stream_ptr(self.stream)
+
+    def reset(self, graph_ids=None, spins=None, mask=None, seed=0):
+        if graph_ids is not None:
+            gi = torch.as_tensor(graph_ids, dtype=torch.int32, device=self.graphs.device)
+            if mask is None:
+                self.graph_ids.copy_(gi)
+            else:
+                m = torch.as_tensor(mask, device=self.graphs.device).bool()
+                self.graph_ids[m] = gi[m]
+        sp = None
+        if spins is not None:
+            sp = torch.as_tensor(spins, dtype=torch.int8, device=self.graphs.device).contiguous()
+        mk = None
+        if mask is not None:
+            mk = torch.as_tensor(mask, dtype=torch.uint8, device=self.graphs.device).contiguous()
+        _lib.check(_lib.lib.eco_env_reset(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
+                                          _lib.ptr(self.state), self.n_envs, _lib.ptr(self.graph_ids),
+                                          _lib.ptr(sp), _lib.ptr(mk), ctypes.c_uint64(seed),
+                                          _lib.ptr(self.obs_x), _lib.ptr(self.obs_f64), self._s()))
+        if mask is None:
+            self.dones.zero_()
+        else:
+            self.dones[mk.bool()] = 0
+        return self.obs_x
+
+    def step(self, actions):
+        a = actions if actions.dtype == torch.int32 else actions.to(torch.int32)
+        _lib.check(_lib.lib.eco_env_step(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
+                                         _lib.ptr(self.state), self.n_envs, _lib.ptr(a.contiguous()),
+                                         _lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.obs_x),
+                                         _lib.ptr(self.obs_f64), self._s()))
+        return self.obs_x, self.rewards, self.dones
+
+    def check_errors(self):
+        _lib.check(_lib.lib.eco_check_errors(self._s()))
+
+    def read(self, spins=False, best_spins=False):
+        """-> dict of per-episode attributes (dqn.py:564-566 BEST metric reads best_score/best_solution)."""
+        dev = self.graphs.device
+        sp = torch.zeros(self.n_envs, self.n_spins, dtype=torch.int8, device=dev) if spins else None
+        bs = torch.zeros(self.n_envs, self.n_spins, dtype=torch.int8, device=dev) if best_spins else None
+        _lib.check(_lib.lib.eco_env_read(ctypes.byref(self.cfg), _lib.ptr(self.state), self.n_envs,
+                                         _lib.ptr(self.scalars), _lib.ptr(sp), _lib.ptr(bs), self._s()))
+        s = self.scalars
+        out = dict(current_step=s[:, 0], score=s[:, 1], normalized_score=s[:, 2], best_score=s[:, 3],
+                   best_score_normalized=s[:, 4], best_solution=s[:, 5], hamming=s[:, 6], done=s[:, 7])
+        if spins:
+            out["spins"] = sp
+        if best_spins:
+            out["best_spins"] = bs
+        return out
+
+    def allowed_action_value(self):
+        """get_allowed_action_states (spinsystem.py:576-593) for irreversible envs: the
+        feature-0 value of still-flippable vertices."""
+        return 0.0 if self.spin_basis == SpinBasis.BINARY else -1.0

@@ -1,0 +1,139 @@
+"""Device graph store: G graphs of N vertices as CSR (eco_graph_set, include/eco_hip.h).
+
+Replaces the dense `GraphGenerator.get() -> ndarray[N,N] f64` adjacency that the
+reference stacks under every observation (spinsystem.py:561-574): on the device a
+graph is CSR with integer weights, shared by every episode that references its id.
+Host-side construction is numpy (input preparation, not the hot path); the
+normalisers (mlr, qn, lb, degrees) are computed on the device by
+eco_graphs_prepare.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _pack_edges(cols, weights):
+    w = np.asarray(weights)
+    if not np.all(np.equal(np.mod(w, 1), 0)) or w.min(initial=0) < -128 or w.max(initial=0) > 127:
+        raise ValueError("eco_hip graphs take integer edge weights in [-128, 127] "
+                         "(EdgeType.UNIFORM / DISCRETE); EdgeType.RANDOM is not supported on the device")
+    return (np.asarray(cols, dtype=np.uint32) | ((w.astype(np.int64) & 0xFF).astype(np.uint32) << 24)).astype(np.uint32)
+
+
+def dense_to_csr(matrices):
+    """list of [N,N] symmetric zero-diagonal matrices -> (row_ptr [G][N+1], edge_base [G], edges)."""
+    mats = [np.asarray(m) for m in matrices]
+    n = mats[0].shape[0]
+    row_ptr = np.zeros((len(mats), n + 1), dtype=np.int32)
+    bases = np.zeros(len(mats), dtype=np.int64)
+    chunks = []
+    off = 0
+    for g, m in enumerate(mats):
+        if m.shape != (n, n):
+            raise ValueError("all graphs in a store must have the same N")
+        if np.any(np.diag(m) != 0):
+            raise ValueError("adjacency must have a zero diagonal (src/envs/utils.py:198-199)")
+        if not np.array_equal(m, m.T):
+            raise ValueError("adjacency must be symmetric (unbiased MaxCut)")
+        r, c = np.nonzero(m)
+        row_ptr[g, 1:] = np.cumsum(np.bincount(r, minlength=n))
+        bases[g] = off
+        chunks.append(_pack_edges(c, m[r, c]))
+        off += r.size
+    edges = np.concatenate(chunks) if chunks else np.zeros(0, np.uint32)
+    return row_ptr, bases, edges
+
+
+def random_csr(kind, n_graphs, n, param, seed, weights="discrete", chunk=512):
+    """Seeded synthetic graph pool built directly as CSR (no dense N x N per graph).
+    kind 'ER': G(n, p=param); 'BA': preferential attachment with m=param.
+    weights 'discrete' = fair +-1 per edge (EdgeType.DISCRETE), 'uniform' = 1."""
+    rng = np.random.default_rng(seed)
+    row_ptr = np.zeros((n_graphs, n + 1), dtype=np.int32)
+    bases = np.zeros(n_graphs, dtype=np.int64)
+    parts = []
+    off = 0
+    iu_all, ju_all = np.triu_indices(n, 1)
+    for g0 in range(0, n_graphs, chunk):
+        g1 = min(n_graphs, g0 + chunk)
+        for g in range(g0, g1):
+            if kind == "ER":
+                keep = rng.random(iu_all.size) < param
+                iu, ju = iu_all[keep], ju_all[keep]
+            elif kind == "BA":
+                iu, ju = _ba_edges(n, int(param), rng)
+            else:
+                raise ValueError(kind)
+            w = (2 * rng.integers(0, 2, iu.size) - 1) if weights == "discrete" else np.ones(iu.size, np.int64)
+            r = np.concatenate([iu, ju])
+            c = np.concatenate([ju, iu])
+            ww = np.concatenate([w, w])
+            order = np.lexsort((c, r))
+            r, c, ww = r[order], c[order], ww[order]
+            row_ptr[g, 1:] = np.cumsum(np.bincount(r, minlength=n))
+            bases[g] = off
+            parts.append(_pack_edges(c, ww))
+            off += r.size
+    return row_ptr, bases, np.concatenate(parts)
+
+
+def _ba_edges(n, m, rng):
+    targets = list(range(m))
+    repeated = []
+    iu, ju = [], []
+    for src in range(m, n):
+        iu.extend(targets)
+        ju.extend([src] * m)
+        repeated.extend(targets)
+        repeated.extend([src] * m)
+        chosen = set()
+        while len(chosen) < m:
+            chosen.add(repeated[int(rng.integers(0, len(repeated)))])
+        targets = sorted(chosen)
+    return np.array(iu, dtype=np.int64), np.array(ju, dtype=np.int64)
+
+
+class GraphStore:
+    """G graphs of N vertices resident on the device (eco_graph_set)."""
+
+    def __init__(self, row_ptr, edge_base, edges, device="cuda", stream=None):
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+        self.n_graphs, n1 = row_ptr.shape
+        self.n_spins = n1 - 1
+        if self.n_spins > _lib.ECO_MAX_SPINS:
+            raise ValueError(f"N={self.n_spins} exceeds ECO_MAX_SPINS={_lib.ECO_MAX_SPINS}")
+        dev = torch.device(device)
+        self.device = dev
+        self.row_ptr = torch.from_numpy(row_ptr).to(dev)
+        self.edge_base = torch.from_numpy(np.ascontiguousarray(edge_base, dtype=np.int64)).to(dev)
+        e = np.ascontiguousarray(edges, dtype=np.uint32).view(np.int32)
+        self.edges = torch.from_numpy(e if e.size else np.zeros(1, np.int32)).to(dev)
+        self.deg = torch.zeros(self.n_graphs, self.n_spins, dtype=torch.int32, device=dev)
+        self.max_deg = torch.zeros(self.n_graphs, dtype=torch.int32, device=dev)
+        self.meta = torch.zeros(self.n_graphs, 4, dtype=torch.float64, device=dev)
+        self.valid = torch.zeros(self.n_graphs, dtype=torch.int32, device=dev)
+        self.gs = _lib.GraphSet(self.n_graphs, self.n_spins, self.row_ptr.data_ptr(), self.edge_base.data_ptr(),
+                                self.edges.data_ptr(), self.deg.data_ptr(), self.max_deg.data_ptr(),
+                                self.meta.data_ptr(), self.valid.data_ptr())
+        _lib.check(_lib.lib.eco_graphs_prepare(ctypes.byref(self.gs), _lib.stream_ptr(stream)))
+
+    @classmethod
+    def from_dense(cls, matrices, device="cuda"):
+        return cls(*dense_to_csr(matrices), device=device)
+
+    @classmethod
+    def random(cls, kind, n_graphs, n, param, seed=0, weights="discrete", device="cuda"):
+        return cls(*random_csr(kind, n_graphs, n, param, seed, weights), device=device)
+
+    def dense(self, g):
+        """Host dense adjacency of graph g (for the reference-format observation)."""
+        rp = self.row_ptr[g].cpu().numpy()
+        b = int(self.edge_base[g].item())
+        e = self.edges[b:b + int(rp[-1])].cpu().numpy().view(np.uint32)
+        m = np.zeros((self.n_spins, self.n_spins))
+        rows = np.repeat(np.arange(self.n_spins), np.diff(rp))
+        m[rows, e & 0xFFFFFF] = ((e >> 24).astype(np.uint8)).view(np.int8)
+        return m

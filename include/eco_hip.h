@@ -1,0 +1,182 @@
+/*
+ * eco_hip.h -- C ABI of libecohip.so, the MI355X (gfx950) engine behind the
+ * ECO-DQN MaxCut hot path.
+ *
+ * The reference (BetterBelle/eco-dqn) is pure Python with no FFI: its boundary is
+ * the Python API.  Each entry point below replaces one reference
+ * interface, cited as file:line under the reference tree.  The Python host
+ * package (eco-dqn_amd/eco_hip) binds these through ctypes and keeps the
+ * reference's class/method names; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Every buffer is caller-owned DEVICE memory (PyTorch tensors used as plain
+ *     containers: pass tensor.data_ptr()).  The library never allocates or frees
+ *     caller memory; scratch is sized by the *_bytes queries.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); NULL
+ *     means the default stream.  All calls are stream-ordered and asynchronous.
+ *   - Every function returns ECO_OK (0) or an error code; eco_last_error() gives
+ *     a thread-local message.  Host-side argument errors are reported before any
+ *     launch.
+ *   - Batched envs that are done are auto-masked: stepping them changes nothing
+ *     and `dones` stays 1 until they are reset (the reference never steps a done
+ *     env in its batched loops, experiments/utils.py:183-201, dqn.py:558-600).
+ */
+#ifndef ECO_HIP_H
+#define ECO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *eco_stream_t; /* hipStream_t */
+
+/* ---- status codes; the Python wrapper maps them to the reference's exceptions ---- */
+enum {
+  ECO_OK = 0,
+  ECO_ERR_ARG = 1,         /* bad argument (ValueError) */
+  ECO_ERR_HIP = 2,         /* HIP runtime error */
+  ECO_ERR_PAST_END = 3,    /* step after done: NotImplementedError, spinsystem.py:365-367 */
+  ECO_ERR_BASIS = 4,       /* unknown spin basis: Exception, spinsystem.py:600-606 */
+  ECO_ERR_TARGET = 5,      /* unsupported optimisation target: NotImplementedError, score_solver.py:885 */
+  ECO_ERR_OBSERVABLE = 6,  /* first observable != SPIN_STATE: AssertionError, spinsystem.py:116 */
+  ECO_ERR_GRAPH = 7        /* graph with no nonzero local reward (spinsystem.py:203-211) or bad CSR */
+};
+
+/* ---- enums: numerically identical to src/envs/utils.py:10-66 ---- */
+enum { ECO_OBS_SPIN_STATE = 1, ECO_OBS_IMMEDIATE_QUALITY_CHANGE = 2, ECO_OBS_IMMEDIATE_VALIDITY_DIFFERENCE = 3,
+       ECO_OBS_IMMEDIATE_VALIDITY_CHANGE = 4, ECO_OBS_TIME_SINCE_FLIP = 5, ECO_OBS_EPISODE_TIME = 6,
+       ECO_OBS_TERMINATION_IMMANENCY = 7, ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS = 8,
+       ECO_OBS_NUMBER_OF_VALIDITY_IMPROVEMENTS = 9, ECO_OBS_DISTANCE_FROM_BEST_SOLUTION = 10,
+       ECO_OBS_DISTANCE_FROM_BEST_STATE = 11, ECO_OBS_GLOBAL_VALIDITY_DIFFERENCE = 12, ECO_OBS_VALIDITY_BIT = 13 };
+enum { ECO_REWARD_DENSE = 1, ECO_REWARD_BLS = 2, ECO_REWARD_SINGLE = 3, ECO_REWARD_CUSTOM_BLS = 4 };
+enum { ECO_BASIS_SIGNED = 1, ECO_BASIS_BINARY = 2 };
+enum { ECO_STOP_NORMAL = 1, ECO_STOP_QUARTER = 2, ECO_STOP_EARLY = 3 };
+
+#define ECO_MAX_OBS 8      /* observables per node (obs_x rows are padded to 8 floats) */
+#define ECO_MAX_SPINS 2048 /* largest N the env kernels take (wave-per-episode, 32 vertices per lane) */
+
+/* Env configuration: the kwargs of core.make("SpinSystem", gg, max_steps, **env_args)
+ * (src/envs/core.py:3-10 -> spinsystem.py:29-48).  Only OptimisationTarget.CUT,
+ * unbiased graphs, ExtraAction.NONE and memory_length=None are on the hot path. */
+typedef struct {
+  int32_t n_spins;                /* N */
+  int32_t max_steps;              /* T */
+  int32_t n_obs;                  /* number of observables, 1..8 */
+  int32_t obs_ids[ECO_MAX_OBS];   /* Observable values; obs_ids[0] == SPIN_STATE */
+  int32_t reward_signal;          /* ECO_REWARD_* */
+  int32_t norm_rewards;           /* bool */
+  int32_t reversible_spins;       /* bool */
+  int32_t spin_basis;             /* ECO_BASIS_* (observation row 0 only) */
+  int32_t stopping;               /* ECO_STOP_* */
+  int32_t has_basin_reward;       /* basin_reward is not None */
+  int32_t has_stag_punishment;    /* stag_punishment is not None */
+  int32_t horizon_length;         /* horizon_length, or max_steps when None (spinsystem.py:163) */
+  double basin_reward;
+  double stag_punishment;
+} eco_env_config;
+
+/* A set of G graphs with N vertices each, as CSR on the device.
+ * Replaces GraphGenerator.get() -> ndarray[N,N] (src/envs/utils.py:121-123): the
+ * dense f64 adjacency is never materialised on the hot path.
+ * Filled by the caller: n_graphs, n_spins, row_ptr, edge_base, edges.
+ * Filled by eco_graphs_prepare: deg, max_deg, meta, valid. */
+typedef struct {
+  int32_t n_graphs;
+  int32_t n_spins;
+  const int32_t *row_ptr;   /* [G][N+1] edge offsets local to each graph */
+  const int64_t *edge_base; /* [G] offset of graph g's first edge in `edges` */
+  const uint32_t *edges;    /* packed edge: column | ((uint8_t)weight << 24); integer weights in [-128,127] */
+  int32_t *deg;             /* [G][N] number of nonzero entries per row (mpnn.py:34-38, before the 0->1 clamp) */
+  int32_t *max_deg;         /* [G] max over rows of max(deg,1) */
+  double *meta;             /* [G][4]: max_local_reward, quality_normalizer, lower_bound, sum(J) */
+  int32_t *valid;           /* [G] 1 if the graph has a nonzero local reward */
+} eco_graph_set;
+
+/* Graph metadata: MaximumCutUnbiasedScorer normalisers (score_solver.py:347-375)
+ * and the MPNN degree normalisation (mpnn.py:34-38), computed on the device. */
+int eco_graphs_prepare(eco_graph_set *gs, eco_stream_t stream);
+
+/* ---- batched SpinSystem (spinsystem.py) ---- */
+
+/* Bytes of the opaque per-batch env state buffer (spins, local fields, counters,
+ * best-so-far, visited-state sets). */
+size_t eco_env_state_bytes(const eco_env_config *cfg, int32_t batch);
+
+/* SpinSystemBase.reset (spinsystem.py:183-259, _reset_state :283-330).
+ * graph_ids[B]: graph of each episode.  spins[B][N] (int8, signed +-1) or NULL:
+ * NULL draws uniform +-1 spins from a counter-based generator keyed by
+ * (seed, episode) (reversible) or all -1 (irreversible, :295-297).
+ * reset_mask[B] or NULL (= all): only episodes with mask != 0 are reset.
+ * `state` must be zero-filled before its first reset.
+ * Outputs (each may be NULL): obs_x[B][N][8] fp32 node features as the MPNN reads
+ * them (obs.float(), dqn.py:282), obs_f64[B][n_obs][N] the reference's float64
+ * observation rows (get_observation :561-574 without the appended adjacency). */
+int eco_env_reset(const eco_env_config *cfg, const eco_graph_set *gs, void *state, int32_t batch,
+                  const int32_t *graph_ids, const int8_t *spins, const uint8_t *reset_mask, uint64_t seed,
+                  float *obs_x, double *obs_f64, eco_stream_t stream);
+
+/* SpinSystemBase.step (spinsystem.py:355-559) for every episode at once.
+ * actions[B] int32 in [0,N); rewards[B] f64; dones[B] u8; obs as in reset. */
+int eco_env_step(const eco_env_config *cfg, const eco_graph_set *gs, void *state, int32_t batch,
+                 const int32_t *actions, double *rewards, uint8_t *dones, float *obs_x, double *obs_f64,
+                 eco_stream_t stream);
+
+/* Read-out of the env attributes callers use (dqn.py:564-566, experiments/utils.py:194-197):
+ * scalars[B][8] = {current_step, score, normalized_score, best_score,
+ *                  best_score_normalized, best_solution, hamming_to_best, done};
+ * spins / best_spins [B][N] int8 signed (each may be NULL). */
+int eco_env_read(const eco_env_config *cfg, const void *state, int32_t batch, double *scalars, int8_t *spins,
+                 int8_t *best_spins, eco_stream_t stream);
+
+/* ---- MPNN Q-network (src/networks/mpnn.py) ---- */
+
+/* Parameter count of MPNN(n_obs_in, n_layers=3, n_features=64, n_hid_readout=[])
+ * in state_dict order (58,425 for n_obs_in = 7). */
+size_t eco_mpnn_param_count(int32_t n_obs_in);
+/* Floats of the kernel-side packed parameter image. */
+size_t eco_mpnn_packed_count(void);
+/* Re-pack the flat state_dict-ordered parameters into the kernel image
+ * (after load_state_dict and after every optimiser step). */
+int eco_mpnn_pack(const float *params, int32_t n_obs_in, float *packed, eco_stream_t stream);
+
+/* Norm-max scope of EdgeAndNodeEmbeddingLayer (mpnn.py:102): */
+enum { ECO_NORM_PER_GRAPH = 0, /* B=1 semantics: act (dqn.py:282) */
+       ECO_NORM_PER_CALL = 1   /* max over the whole call: train_step / batched eval */ };
+
+/* epsilon-greedy act fused into the forward (dqn.py:453-465, predict :490-512).
+ * action = random with probability epsilon (uniform over allowed vertices),
+ * else the first argmax of Q over allowed vertices. Irreversible envs allow only
+ * vertices whose node feature 0 equals allowed_value (dqn.py:462-464, :505-511). */
+typedef struct {
+  float epsilon;
+  int32_t reversible;      /* 1: every vertex allowed */
+  float allowed_value;     /* irreversible: feature-0 value of flippable vertices */
+  uint64_t seed;
+  uint64_t counter;        /* advance per call; (seed, counter, episode) keys the draws */
+} eco_act_config;
+
+size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch);
+
+/* MPNN.forward (mpnn.py:40-77) on B graphs at once.
+ * obs_x[B][N][8]: node features; adjacency = graphs graph_ids[B] of `gs`.
+ * q[B][N] fp32 (may be NULL when only actions are wanted).
+ * act / actions[B]: optional fused epsilon-greedy action selection. */
+int eco_mpnn_forward(const float *packed, int32_t n_obs_in, const eco_graph_set *gs, const int32_t *graph_ids,
+                     int32_t batch, const float *obs_x, int32_t norm_scope, float *q, const eco_act_config *act,
+                     int32_t *actions, void *workspace, eco_stream_t stream);
+
+/* Device-side errors (bad action, invalid graph, non-signed injected spins) are
+ * recorded in a device word by the asynchronous kernels; this synchronises
+ * `stream`, returns and clears the first one (ECO_OK if none). */
+int eco_check_errors(eco_stream_t stream);
+
+/* Thread-local text of the last error. */
+const char *eco_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECO_HIP_H */
