@@ -99,10 +99,12 @@ struct ObsCtx {
   double mlr, dist_best, hamming, nqi, term, ep_time;
   int basis;
 };
-__device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int g, int tsfk, const double* tab) {
+// g is passed as the field h; the reference's g = s * (J@s) is a float64 product, so
+// s = -1 with h = +0.0 gives -0.0 (kept: observations are compared bitwise).
+__device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int h, int tsfk, const double* tab) {
   switch (id) {
     case ECO_OBS_SPIN_STATE: return c.basis == ECO_BASIS_BINARY ? (double)(1 - s) / 2.0 : (double)s;
-    case ECO_OBS_IMMEDIATE_QUALITY_CHANGE: return (double)g / c.mlr;
+    case ECO_OBS_IMMEDIATE_QUALITY_CHANGE: return ((double)s * (double)h) / c.mlr;
     case ECO_OBS_TIME_SINCE_FLIP: return tab[tsfk];
     case ECO_OBS_EPISODE_TIME: return c.ep_time;
     case ECO_OBS_TERMINATION_IMMANENCY: return c.term;
@@ -116,7 +118,7 @@ __device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int 
 }
 
 template <int VPT>
-__device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, const int (&s)[VPT], const int (&g)[VPT],
+__device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, const int (&s)[VPT], const int (&h)[VPT],
                                           const int (&tsf)[VPT], const ObsCtx& c) {
   const int N = a.cfg.n_spins;
   const int nobs = a.cfg.n_obs;
@@ -130,7 +132,7 @@ __device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, con
     for (int i = 0; i < ECO_MAX_OBS; ++i) {
       double val = 0.0;
       if (i < nobs) {
-        val = obs_value(a.cfg.obs_ids[i], c, s[k], g[k], tsf[k], tab);
+        val = obs_value(a.cfg.obs_ids[i], c, s[k], h[k], tsf[k], tab);
         if (a.obs_f64) a.obs_f64[((size_t)e * nobs + i) * N + v] = val;
       }
       xf[i] = (float)val;
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
   ObsCtx c;
   c.mlr = mlr; c.dist_best = 0.0; c.hamming = 0.0; c.nqi = (double)cnt / (double)N;
   c.term = 0.0; c.ep_time = 0.0; c.basis = a.cfg.spin_basis;
-  write_obs<VPT>(a, e, lane, s, g, tsf, c);
+  write_obs<VPT>(a, e, lane, s, h, tsf, c);
 }
 
 // SpinSystemBase.step (spinsystem.py:355-559), ExtraAction.NONE, memory_length None.
@@ -262,9 +264,8 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   int16_t* gt = (int16_t*)(a.state + L.off_tsf) + (size_t)e * N;
   int8_t* gb = (int8_t*)(a.state + L.off_best) + (size_t)e * N;
   const int sa_old = gsp[act];
-  const int delta_i = sa_old * gh[act];  // get_score_mask(state)[action] (:393)
   const double qn = sc->qn, mlr = sc->mlr;
-  const double delta = (double)delta_i;
+  const double delta = (double)sa_old * (double)gh[act];  // f64 product: keeps -0.0 like the reference
   const double delta_n = delta / qn;     // get_normalized_score_mask(state)[action] (:394)
   const double score = sc->score + delta;           // :399
   const double nscore = sc->nscore + delta_n;       // :400 (accumulated)
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   c.term = x > 0.0 ? x : 0.0;                                         // :509-511
   c.ep_time = tab_ptr(a)[t];                                          // :506
   c.basis = a.cfg.spin_basis;
-  write_obs<VPT>(a, e, lane, s, g, tsf, c);
+  write_obs<VPT>(a, e, lane, s, h, tsf, c);
 }
 
 // read-out of episode scalars / spins

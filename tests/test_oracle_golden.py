@@ -59,7 +59,7 @@ def test_env_er20_bit_exact():
         ref = f[p + "obs"]
 
         def check(t, o):
-            np.testing.assert_array_equal(o, ref[t])
+            np.testing.assert_array_equal(o.view(np.uint64), ref[t].view(np.uint64))  # bitwise (signed zeros)
         _run(f, p, check)
 
 
