@@ -1,5 +1,5 @@
-// MPNN Q-network forward (src/networks/mpnn.py) fused per graph block on gfx950,
-// with the epsilon-greedy act (dqn.py:453-465, :490-512) fused into the readout.
+// MPNN Q-network (src/networks/mpnn.py) forward + backward, fused per graph block on
+// gfx950, with the epsilon-greedy act (dqn.py:453-465, :490-512) fused into the readout.
 //
 // One 256-thread workgroup (4 waves) owns a block of whole graphs (graphs_per_block
 // = max(1, 256/N)); the block's node embeddings H [rows][64] fp32 live in LDS for
@@ -12,54 +12,47 @@
 //     16-byte loads: MFMA kk of a 16-wide k chunk takes k = 16c + 4(l>>4) + kk;
 //   * the edge layer never builds the [N,N,63] edge tensor (mpnn.py:90-100): with
 //     Z = Wx.x per node in LDS, relu(We.[A_ij, x_j]) = relu(A_ij*w_a + Z_j) per edge.
+// The backward (autograd of the same graph, dqn.py:440-449) mirrors it: activation
+// gradients per block (A^T.x aggregations are gathers because A is symmetric), weight
+// gradients as separate split-K reductions over all nodes (eco_train.hip).
 #include "eco_common.h"
+#include "eco_mpnn.h"
 
 namespace eco {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// ---- packed parameter image (floats) ----
-constexpr int PK_W0 = 0;                   // [64][8]  node_init_embedding (cols >= n_obs zero)
-constexpr int PK_WX = 512;                 // [64][8]  edge_embedding_NN.weight[:, 1:] (row 63 zero)
-constexpr int PK_WA = 1024;                // [64]     edge_embedding_NN.weight[:, 0]  ([63] = 0)
-constexpr int PK_WF = 1088;                // [64][64] edge_feature_NN
-constexpr int PK_LAYER = 5184;             // + l*16384: message [64][128], +8192: update [64][128]
-constexpr int PK_WP = PK_LAYER + 3 * 16384;  // [64][64] layer_pooled
-constexpr int PK_WR = PK_WP + 4096;        // [128] layers_readout.0.weight
-constexpr int PK_BR = PK_WR + 128;         // [1]   layers_readout.0.bias
-constexpr int PK_TOTAL = PK_BR + 64;
-
-constexpr int LDH = 68;   // LDS row stride (floats) of node-embedding tiles: 16 rows -> distinct bank quads
-constexpr int NWAVE = 4;
-constexpr int TPB = 64 * NWAVE;
-
-__host__ __device__ inline int flat_count(int nobs) { return 64 * nobs + 63 * (1 + nobs) + 4096 + 6 * 8192 + 4096 + 128 + 1; }
 
 __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= PK_TOTAL) return;
-  const int oW0 = 0, oWe = 64 * nobs, oWf = oWe + 63 * (1 + nobs), oL = oWf + 4096, oWp = oL + 6 * 8192;
-  const int oWr = oWp + 4096, oBr = oWr + 128;
+  const FlatOffsets o = flat_offsets(nobs);
   float v = 0.f;
   if (i < PK_WX) {
     const int r = i >> 3, c = i & 7;
-    v = c < nobs ? f[oW0 + r * nobs + c] : 0.f;
+    v = c < nobs ? f[o.W0 + r * nobs + c] : 0.f;
   } else if (i < PK_WA) {
     const int r = (i - PK_WX) >> 3, c = (i - PK_WX) & 7;
-    v = (r < 63 && c < nobs) ? f[oWe + r * (1 + nobs) + 1 + c] : 0.f;
+    v = (r < 63 && c < nobs) ? f[o.We + r * (1 + nobs) + 1 + c] : 0.f;
   } else if (i < PK_WF) {
     const int r = i - PK_WA;
-    v = r < 63 ? f[oWe + r * (1 + nobs)] : 0.f;
+    v = r < 63 ? f[o.We + r * (1 + nobs)] : 0.f;
   } else if (i < PK_LAYER) {
-    v = f[oWf + (i - PK_WF)];
+    v = f[o.Wf + (i - PK_WF)];
   } else if (i < PK_WP) {
-    v = f[oL + (i - PK_LAYER)];  // message0, update0, message1, ... same order as state_dict
+    v = f[o.L + (i - PK_LAYER)];  // message0, update0, message1, ... same order as state_dict
   } else if (i < PK_WR) {
-    v = f[oWp + (i - PK_WP)];
+    v = f[o.Wp + (i - PK_WP)];
   } else if (i < PK_BR) {
-    v = f[oWr + (i - PK_WR)];
+    v = f[o.Wr + (i - PK_WR)];
   } else if (i == PK_BR) {
-    v = f[oBr];
+    v = f[o.Br];
+  } else if (i >= PK_WFT && i < PK_LAYERT) {
+    const int j = i - PK_WFT;  // WfT[in][out] = Wf[out][in]
+    v = f[o.Wf + (j & 63) * 64 + (j >> 6)];
+  } else if (i >= PK_LAYERT && i < PK_LAYERT + 3 * 16384) {
+    const int l = (i - PK_LAYERT) / 16384;
+    const int j = (i - PK_LAYERT) % 16384;
+    const int which = j / 8192;  // 0: message, 1: update
+    const int jj = j % 8192;     // T[in (128)][out (64)]
+    v = f[o.L + l * 16384 + which * 8192 + (jj & 63) * 128 + (jj >> 6)];
   }
   p[i] = v;
 }
@@ -73,20 +66,25 @@ struct MpnnArgs {
   int norm_scope;
   const int* call_maxdeg;
   float* q;              // [B*N] or null
-  float* E;              // workspace [B*N][64]
+  float* E;              // [B*N][64] (workspace, or the saved E tensor)
+  float* sv;             // saved activations (training forward) or null
   int has_act;
   eco_act_config act;
   int32_t* actions;
+  // backward
+  const float* dq;       // [B*N]
+  float* gr;             // gradient workspace
 };
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
 // acc[nt] += A(16 rows x 16 k, one float4 per lane) * W[nt*16 + (l&15)][kbase + 4(l>>4) + 0..3]
-__device__ __forceinline__ void mm_chunk(f32x4 (&acc)[4], float4 a, const float* __restrict__ W, int ldw, int kbase,
+template <int NT>
+__device__ __forceinline__ void mm_chunk(f32x4 (&acc)[NT], float4 a, const float* __restrict__ W, int ldw, int kbase,
                                          int lane) {
   const float* wp = W + (lane & 15) * ldw + kbase + 4 * (lane >> 4);
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+  for (int nt = 0; nt < NT; ++nt) {
     const float4 b = *reinterpret_cast<const float4*>(wp + nt * 16 * ldw);
     acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[nt], 0, 0, 0);
     acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[nt], 0, 0, 0);
@@ -100,6 +98,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+__device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 struct NodeRef {
   bool valid;
@@ -123,7 +125,32 @@ __device__ __forceinline__ NodeRef node_ref(const MpnnArgs& a, int blk, int r, i
   return n;
 }
 
-template <int MAXT>
+__device__ __forceinline__ int node_norm(const MpnnArgs& a, int blk, int r, int rows_valid) {
+  if (r >= rows_valid) return 1;
+  const int gl = r / a.N;
+  const int gid = a.gids[blk * a.gpb + gl];
+  return max(a.gs.deg[(size_t)gid * a.N + (r - gl * a.N)], 1);
+}
+
+// Sum over the CSR row of node n of w * S[j][16c + 4(l>>4) + 0..3] (S: LDS, row stride LDH).
+__device__ __forceinline__ void gather_rows(const NodeRef& n, const float* S, int N, int s4, float4 (&acc)[4]) {
+  const int rbase = n.gl * N;
+  for (int q = n.e0; q < n.e1; ++q) {
+    const uint32_t ex = n.ed[q];
+    const float wv = (float)edge_w(ex);
+    const float* hr = S + (rbase + edge_col(ex)) * LDH + 4 * s4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 hv = f4(hr + 16 * c);
+      acc[c].x = fmaf(wv, hv.x, acc[c].x);
+      acc[c].y = fmaf(wv, hv.y, acc[c].y);
+      acc[c].z = fmaf(wv, hv.z, acc[c].z);
+      acc[c].w = fmaf(wv, hv.w, acc[c].w);
+    }
+  }
+}
+
+template <int MAXT, bool SAVE>
 __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
@@ -137,6 +164,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   float* Hs = lds;                                  // [rows_pad][LDH]
   float* Ms = lds + rows_pad * LDH + w * 16 * LDH;  // per-wave [16][LDH]
   const size_t R0 = (size_t)blk * a.gpb * N;        // first global row of the block
+  const size_t RT = (size_t)a.B * N;                // rows of the call
   const float* P = a.P;
   const int s4 = lane >> 4;
 
@@ -158,7 +186,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   }
   __syncthreads();
 
-  // ---- phase B: edge embedding (mpnn.py:89-104) -> E (global workspace) ----
+  // ---- phase B: edge embedding (mpnn.py:89-104) -> E ----
   {
     int maxdeg_call = 0;
     if (a.norm_scope == ECO_NORM_PER_CALL) maxdeg_call = *a.call_maxdeg;
@@ -172,7 +200,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
       const NodeRef n = node_ref(a, blk, r, rows_valid);
       float4 acc[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int c = 0; c < 4; ++c) acc[c] = zero4();
       const int rbase = n.gl * N;
       for (int q = n.e0; q < n.e1; ++q) {
         const uint32_t ex = n.ed[q];
@@ -180,7 +208,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         const float* zr = Hs + (rbase + edge_col(ex)) * LDH + 4 * s4;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float4 z = *reinterpret_cast<const float4*>(zr + 16 * c);
+          const float4 z = f4(zr + 16 * c);
           acc[c].x += relu(fmaf(wv, wa[4 * c + 0], z.x));
           acc[c].y += relu(fmaf(wv, wa[4 * c + 1], z.y));
           acc[c].z += relu(fmaf(wv, wa[4 * c + 2], z.z));
@@ -197,13 +225,17 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
       if (s4 == 3) acc[3].w = nf / (float)md;
       if (!n.valid) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = 0; c < 4; ++c) acc[c] = zero4();
+      } else if (SAVE) {
+        float* ea = a.sv + (size_t)SV_EAGG * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st4(ea + 16 * c, acc[c]);
       }
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) mm_chunk(d, acc[c], P + PK_WF, 64, 16 * c, lane);
+      for (int c = 0; c < 4; ++c) mm_chunk<4>(d, acc[c], P + PK_WF, 64, 16 * c, lane);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = t * 16 + 4 * s4 + rr;
@@ -228,6 +260,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         const float4 x0 = xp[0], x1 = xp[1];
         z = w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x + w0[5] * x1.y + w0[6] * x1.z +
             w0[7] * x1.w;
+        if (SAVE) a.sv[(size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + lane] = relu(z);
       }
       Hs[r * LDH + lane] = relu(z);
     }
@@ -248,53 +281,50 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         // aggregation (A . h) / norm, in A-operand layout
         float4 agg[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) agg[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int rbase = n.gl * N;
-        for (int q = n.e0; q < n.e1; ++q) {
-          const uint32_t ex = n.ed[q];
-          const float wv = (float)edge_w(ex);
-          const float* hr = Hs + (rbase + edge_col(ex)) * LDH + 4 * s4;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float4 hv = *reinterpret_cast<const float4*>(hr + 16 * c);
-            agg[c].x = fmaf(wv, hv.x, agg[c].x);
-            agg[c].y = fmaf(wv, hv.y, agg[c].y);
-            agg[c].z = fmaf(wv, hv.z, agg[c].z);
-            agg[c].w = fmaf(wv, hv.w, agg[c].w);
-          }
-        }
+        for (int c = 0; c < 4; ++c) agg[c] = zero4();
+        gather_rows(n, Hs, N, s4, agg);
         const float nf = (float)n.norm;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           agg[c].x = agg[c].x / nf; agg[c].y = agg[c].y / nf; agg[c].z = agg[c].z / nf; agg[c].w = agg[c].w / nf;
+        }
+        if (SAVE && n.valid) {
+          float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
         }
         // message = relu(Wm . [agg, e])
         f32x4 d[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) mm_chunk(d, agg[c], Wm, 128, 16 * c, lane);
+        for (int c = 0; c < 4; ++c) mm_chunk<4>(d, agg[c], Wm, 128, 16 * c, lane);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          float4 ev = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (n.valid) ev = *reinterpret_cast<const float4*>(a.E + (R0 + r) * 64 + 16 * c + 4 * s4);
-          mm_chunk(d, ev, Wm, 128, 64 + 16 * c, lane);
+          float4 ev = zero4();
+          if (n.valid) ev = f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4);
+          mm_chunk<4>(d, ev, Wm, 128, 64 + 16 * c, lane);
         }
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = t * 16 + 4 * s4 + rr;
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) Ms[(4 * s4 + rr) * LDH + nt * 16 + (lane & 15)] = relu(d[nt][rr]);
+          for (int nt = 0; nt < 4; ++nt) {
+            const float mv = relu(d[nt][rr]);
+            Ms[(4 * s4 + rr) * LDH + nt * 16 + (lane & 15)] = mv;
+            if (SAVE && row < rows_valid)
+              a.sv[(size_t)(SV_M0 + layer) * RT * 64 + (R0 + row) * 64 + nt * 16 + (lane & 15)] = mv;
+          }
+        }
         wave_lds_sync();
         // h' = relu(Wu . [h, m])
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          mm_chunk(hn[ti], *reinterpret_cast<const float4*>(Hs + r * LDH + 16 * c + 4 * s4), Wu, 128, 16 * c, lane);
+        for (int c = 0; c < 4; ++c) mm_chunk<4>(hn[ti], f4(Hs + r * LDH + 16 * c + 4 * s4), Wu, 128, 16 * c, lane);
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          mm_chunk(hn[ti], *reinterpret_cast<const float4*>(Ms + (lane & 15) * LDH + 16 * c + 4 * s4), Wu, 128,
-                   64 + 16 * c, lane);
+          mm_chunk<4>(hn[ti], f4(Ms + (lane & 15) * LDH + 16 * c + 4 * s4), Wu, 128, 64 + 16 * c, lane);
         wave_lds_sync();
       }
     }
@@ -304,9 +334,16 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = t * 16 + 4 * s4 + rr;
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) Hs[(t * 16 + 4 * s4 + rr) * LDH + nt * 16 + (lane & 15)] = relu(hn[ti][nt][rr]);
+          for (int nt = 0; nt < 4; ++nt) {
+            const float hv = relu(hn[ti][nt][rr]);
+            Hs[row * LDH + nt * 16 + (lane & 15)] = hv;
+            if (SAVE && row < rows_valid)
+              a.sv[(size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + row) * 64 + nt * 16 + (lane & 15)] = hv;
+          }
+        }
       }
     }
     __syncthreads();
@@ -324,6 +361,10 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
     const float* wp = P + PK_WP + lane * 64;
 #pragma unroll 8
     for (int k = 0; k < 64; ++k) p = fmaf(wp[k], __shfl(mean, k, 64), p);
+    if (SAVE) {
+      a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)e * 64 + lane] = mean;
+      a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)a.B * 64 + (size_t)e * 64 + lane] = p;
+    }
     const float cg = wave_sum_f(relu(p) * P[PK_WR + lane]);
     float bestq = -INFINITY;
     int besti = 0x7fffffff;
@@ -337,7 +378,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         float ql = 0.f;
 #pragma unroll 4
         for (int f = 0; f < 64; f += 4) {
-          const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+          const float4 hv = f4(hr + f);
           ql = fmaf(hv.x, P[PK_WR + 64 + f], ql);
           ql = fmaf(hv.y, P[PK_WR + 65 + f], ql);
           ql = fmaf(hv.z, P[PK_WR + 66 + f], ql);
@@ -366,8 +407,7 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         if (a.act.reversible) {
           action = k;
         } else {
-          // k-th allowed vertex
-          action = -1;
+          action = -1;  // k-th allowed vertex
           for (int v0 = 0; v0 < N && action < 0; v0 += 64) {
             const int v = v0 + lane;
             const bool al = v < N && a.x[((size_t)e * N + v) * 8] == a.act.allowed_value;
@@ -388,6 +428,311 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   }
 }
 
+// ============================================================== backward ====
+// Gradient of loss w.r.t. all MPNN parameters given dq = dLoss/dQ [B][N], for the
+// forward saved in a.sv.  This kernel produces the activation gradients (the
+// pre-activation gradients dY of every Linear, stored [R][64]) and the small
+// per-graph / per-block partials; eco_train.hip reduces dW = sum_nodes dY^T X.
+template <int MAXT>
+__global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  float* G = lds;                                            // [rows_pad][LDH] gathered-gradient source
+  float* Ms = lds + rows_pad * LDH + w * 16 * LDH;           // per-wave transpose scratch
+  float* DMEAN = lds + rows_pad * LDH + NWAVE * 16 * LDH;    // [gpb][64]
+  float* RED = DMEAN + a.gpb * 64;                           // [NWAVE][64] dwa partials
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const float* sv = a.sv;
+  float* gr = a.gr;
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
+  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
+  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
+  const float* PP = MEAN + (size_t)a.B * 64;
+  float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
+  float* DWRA = DP + (size_t)a.B * 64;
+  float* DWRB = DWRA + (size_t)a.B * 64;
+  float* DBR = DWRB + (size_t)a.B * 64;
+  float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
+
+  // ---- readout backward (mpnn.py:143-159) per graph ----
+  for (int gl = w; gl < g_valid; gl += NWAVE) {
+    const int e = blk * a.gpb + gl;
+    const float* dqe = a.dq + (size_t)e * N;
+    float s = 0.f;
+    for (int v = lane; v < N; v += 64) s += dqe[v];
+    const float S = wave_sum_f(s);                       // d(sum_i q_i) / d br ...
+    const float p = PP[(size_t)e * 64 + lane];
+    const float wr = P[PK_WR + lane];
+    const float dp = wr * S * (p > 0.f ? 1.f : 0.f);
+    DP[(size_t)e * 64 + lane] = dp;
+    DWRA[(size_t)e * 64 + lane] = relu(p) * S;
+    if (lane == 0) DBR[e] = S;
+    float dmean = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
+    DMEAN[gl * 64 + lane] = dmean / (float)N;
+    float dwb = 0.f;
+    const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+    for (int v = 0; v < N; ++v) {
+      const float dv = dqe[v];
+      if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+    }
+    DWRB[(size_t)e * 64 + lane] = dwb;
+  }
+  __syncthreads();
+
+  // dh3 (A layout): dq_i * wr[64+f] + dmean_f / N
+  float4 dh[MAXT][4];
+#pragma unroll
+  for (int ti = 0; ti < MAXT; ++ti) {
+    const int t = w + ti * NWAVE;
+    const int r = t * 16 + c16;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dh[ti][c] = zero4();
+    if (t < ntiles && r < rows_valid) {
+      const int gl = r / N;
+      const float dqi = a.dq[R0 + r];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 16 * c + 4 * s4;
+        const float4 dm = f4(DMEAN + gl * 64 + f);
+        dh[ti][c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
+                                fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
+      }
+    }
+  }
+
+  // ---- update layers in reverse (mpnn.py:114-120) ----
+  for (int layer = 2; layer >= 0; --layer) {
+    const float* WmT = P + PK_LAYERT + layer * 16384;  // [128][64]
+    const float* WuT = WmT + 8192;                      // [128][64]
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NWAVE;
+      if (t < ntiles) {
+        const int r = t * 16 + c16;
+        const bool valid = r < rows_valid;
+        // duu = dh' * [h' > 0]
+        float4 duu[4];
+        const float* hnext = SV(SV_H0 + layer + 1) + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 hv = valid ? f4(hnext + 16 * c) : zero4();
+          duu[c] = make_float4(hv.x > 0.f ? dh[ti][c].x : 0.f, hv.y > 0.f ? dh[ti][c].y : 0.f,
+                               hv.z > 0.f ? dh[ti][c].z : 0.f, hv.w > 0.f ? dh[ti][c].w : 0.f);
+          if (valid) st4(GR(GR_DUU0 + layer) + (R0 + r) * 64 + 4 * s4 + 16 * c, duu[c]);
+        }
+        // d[h, m] = duu . Wu  -> [node][128]
+        f32x4 d8[8];
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mm_chunk<8>(d8, duu[c], WuT, 64, 16 * c, lane);
+        // dum = dm * [m > 0]; dh_direct -> DH (global scratch, own rows)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = t * 16 + 4 * s4 + rr;
+          const bool rv = row < rows_valid;
+          const size_t base = (R0 + row) * 64 + c16;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const float mv = rv ? SV(SV_M0 + layer)[base + nt * 16] : 0.f;
+            const float dum = mv > 0.f ? d8[4 + nt][rr] : 0.f;
+            Ms[(4 * s4 + rr) * LDH + nt * 16 + c16] = dum;
+            if (rv) {
+              GR(GR_DUM0 + layer)[base + nt * 16] = dum;
+              GR(GR_DH)[base + nt * 16] = d8[nt][rr];
+            }
+          }
+        }
+        wave_lds_sync();
+        // d[agg, e] = dum . Wm -> [node][128]
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mm_chunk<8>(d8, f4(Ms + c16 * LDH + 16 * c + 4 * s4), WmT, 64, 16 * c, lane);
+        wave_lds_sync();
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = t * 16 + 4 * s4 + rr;
+          const bool rv = row < rows_valid;
+          const float nf = (float)node_norm(a, blk, row, rows_valid);
+          const size_t base = (R0 + row) * 64 + c16;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            G[row * LDH + nt * 16 + c16] = rv ? d8[nt][rr] / nf : 0.f;  // d(agg)/d(A.h) = 1/norm
+            if (rv) {
+              float* de = GR(GR_DE) + base + nt * 16;
+              *de = (layer == 2 ? 0.f : *de) + d8[4 + nt][rr];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NWAVE;
+      if (t < ntiles) {
+        const int r = t * 16 + c16;
+        const NodeRef n = node_ref(a, blk, r, rows_valid);
+        float4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = n.valid ? f4(GR(GR_DH) + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
+        gather_rows(n, G, N, s4, acc);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dh[ti][c] = acc[c];
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- h0 = relu(W0.x): du0 ----
+#pragma unroll
+  for (int ti = 0; ti < MAXT; ++ti) {
+    const int t = w + ti * NWAVE;
+    const int r = t * 16 + c16;
+    if (t < ntiles && r < rows_valid) {
+      const float* h0 = SV(SV_H0) + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 hv = f4(h0 + 16 * c);
+        st4(GR(GR_DU0) + (R0 + r) * 64 + 4 * s4 + 16 * c,
+            make_float4(hv.x > 0.f ? dh[ti][c].x : 0.f, hv.y > 0.f ? dh[ti][c].y : 0.f,
+                        hv.z > 0.f ? dh[ti][c].z : 0.f, hv.w > 0.f ? dh[ti][c].w : 0.f));
+      }
+    }
+  }
+
+  // ---- edge embedding (mpnn.py:89-104): due, dEagg ----
+#pragma unroll
+  for (int ti = 0; ti < MAXT; ++ti) {
+    const int t = w + ti * NWAVE;
+    if (t < ntiles) {
+      const int r = t * 16 + c16;
+      const bool valid = r < rows_valid;
+      float4 due[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const size_t off = (R0 + r) * 64 + 16 * c + 4 * s4;
+        const float4 ev = valid ? f4(SV(SV_E) + off) : zero4();
+        const float4 dv = valid ? f4(GR(GR_DE) + off) : zero4();
+        due[c] = make_float4(ev.x > 0.f ? dv.x : 0.f, ev.y > 0.f ? dv.y : 0.f, ev.z > 0.f ? dv.z : 0.f,
+                             ev.w > 0.f ? dv.w : 0.f);
+        if (valid) st4(GR(GR_DUE) + off, due[c]);
+      }
+      f32x4 d4[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) d4[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mm_chunk<4>(d4, due[c], P + PK_WFT, 64, 16 * c, lane);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = t * 16 + 4 * s4 + rr;
+        const float nf = (float)node_norm(a, blk, row, rows_valid);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) G[row * LDH + nt * 16 + c16] = row < rows_valid ? d4[nt][rr] / nf : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  // dz_j = sum_{i in N(j)} G_i * [w_ij wa + z_j > 0];  dwa += same * w_ij
+  {
+    float wa[16], wx[16][8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * c + 4 * s4 + i;
+        wa[4 * c + i] = P[PK_WA + f];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wx[4 * c + i][k] = P[PK_WX + f * 8 + k];
+      }
+    float dwa[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dwa[i] = 0.f;
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NWAVE;
+      if (t < ntiles) {
+        const int r = t * 16 + c16;
+        const NodeRef n = node_ref(a, blk, r, rows_valid);
+        float xv[8];
+        {
+          const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + (n.valid ? r : 0)) * 8);
+          const float4 x0 = xp[0], x1 = xp[1];
+          xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w; xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
+        }
+        float z[16], dz[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          z[i] = wx[i][0] * xv[0] + wx[i][1] * xv[1] + wx[i][2] * xv[2] + wx[i][3] * xv[3] + wx[i][4] * xv[4] +
+                 wx[i][5] * xv[5] + wx[i][6] * xv[6] + wx[i][7] * xv[7];
+          dz[i] = 0.f;
+        }
+        const int rbase = n.gl * N;
+        for (int q = n.e0; q < n.e1; ++q) {
+          const uint32_t ex = n.ed[q];
+          const float wv = (float)edge_w(ex);
+          const float* gi = G + (rbase + edge_col(ex)) * LDH + 4 * s4;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float4 gv = f4(gi + 16 * c);
+            const float g4[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int k = 4 * c + i;
+              const float gm = fmaf(wv, wa[k], z[k]) > 0.f ? g4[i] : 0.f;
+              dz[k] += gm;
+              dwa[k] = fmaf(gm, wv, dwa[k]);
+            }
+          }
+        }
+        if (n.valid) {
+          float* dzp = GR(GR_DZ) + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) st4(dzp + 16 * c, make_float4(dz[4 * c], dz[4 * c + 1], dz[4 * c + 2], dz[4 * c + 3]));
+        }
+      }
+    }
+    // reduce dwa over the 16 node lanes sharing s4, then over waves (fixed order)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float v = dwa[i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      dwa[i] = v;
+    }
+    if (c16 == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) RED[w * 64 + 16 * c + 4 * s4 + i] = dwa[4 * c + i];
+    }
+    __syncthreads();
+    if (w == 0) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < NWAVE; ++k) s += RED[k * 64 + lane];
+      DWA[(size_t)blk * 64 + lane] = s;
+    }
+  }
+}
+
 __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, int B, int* out) {
   int m = 1;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) m = max(m, gs.max_deg[gids[i]]);
@@ -395,7 +740,20 @@ __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, 
   if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
-static int graphs_per_block(int N) { return N >= 256 ? 1 : 256 / N; }
+static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
+                   const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope) {
+  if (!packed || !gs || !graph_ids || !obs_x) return fail(ECO_ERR_ARG, "null argument");
+  if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
+  if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
+  const int N = gs->n_spins;
+  if (N < 1 || N > MPNN_MAX_SPINS) return fail(ECO_ERR_ARG, "mpnn supports 1 <= N <= 512");
+  if (norm_scope != ECO_NORM_PER_GRAPH && norm_scope != ECO_NORM_PER_CALL)
+    return fail(ECO_ERR_ARG, "bad norm_scope");
+  a = MpnnArgs{};
+  a.P = packed; a.gs = *gs; a.gids = graph_ids; a.B = batch; a.N = N; a.gpb = graphs_per_block(N);
+  a.nobs = n_obs_in; a.x = obs_x; a.norm_scope = norm_scope;
+  return ECO_OK;
+}
 
 }  // namespace eco
 
@@ -403,7 +761,7 @@ using namespace eco;
 
 extern "C" size_t eco_mpnn_param_count(int32_t n_obs_in) {
   if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return 0;
-  return (size_t)flat_count(n_obs_in);
+  return (size_t)flat_offsets(n_obs_in).total;
 }
 
 extern "C" size_t eco_mpnn_packed_count(void) { return (size_t)PK_TOTAL; }
@@ -420,26 +778,35 @@ extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
   return 256 + (size_t)n_spins * batch * 64 * sizeof(float);
 }
 
+extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
+  if (n_spins < 1 || batch < 1) return 0;
+  return ((size_t)SV_NODE_TENSORS * n_spins * batch * 64 + 2 * (size_t)batch * 64) * sizeof(float);
+}
+
+static size_t lds_bytes(int N, int gpb, bool backward) {
+  const int rows_pad = (gpb * N + 15) & ~15;
+  size_t f = (size_t)rows_pad * LDH + (size_t)NWAVE * 16 * LDH;
+  if (backward) f += (size_t)gpb * 64 + NWAVE * 64;
+  return f * sizeof(float);
+}
+
 extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
                                 const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope,
-                                float* q, const eco_act_config* act, int32_t* actions, void* workspace,
+                                float* q, const eco_act_config* act, int32_t* actions, void* saved, void* workspace,
                                 eco_stream_t stream) {
-  if (!packed || !gs || !graph_ids || !obs_x || !workspace) return fail(ECO_ERR_ARG, "null argument");
-  if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
-  if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
-  const int N = gs->n_spins;
-  if (N < 1 || N > 512) return fail(ECO_ERR_ARG, "mpnn_forward supports 1 <= N <= 512");
-  if (norm_scope != ECO_NORM_PER_GRAPH && norm_scope != ECO_NORM_PER_CALL)
-    return fail(ECO_ERR_ARG, "bad norm_scope");
+  MpnnArgs a;
+  int rc = prepare(a, packed, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope);
+  if (rc) return rc;
+  if (!workspace) return fail(ECO_ERR_ARG, "null workspace");
   if (act && !actions) return fail(ECO_ERR_ARG, "act config without actions buffer");
   if (!q && !act) return fail(ECO_ERR_ARG, "nothing to compute (q and act both null)");
   hipStream_t st = (hipStream_t)stream;
-  MpnnArgs a{};
-  a.P = packed; a.gs = *gs; a.gids = graph_ids; a.B = batch; a.N = N; a.gpb = graphs_per_block(N);
-  a.nobs = n_obs_in; a.x = obs_x; a.norm_scope = norm_scope; a.q = q;
+  const int N = a.N;
+  a.q = q;
   int* cmax = (int*)workspace;
   a.call_maxdeg = cmax;
-  a.E = (float*)((char*)workspace + 256);
+  a.sv = (float*)saved;
+  a.E = saved ? a.sv + (size_t)SV_E * batch * N * 64 : (float*)((char*)workspace + 256);
   a.has_act = act != nullptr;
   if (act) a.act = *act;
   a.actions = actions;
@@ -448,15 +815,52 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     call_maxdeg_kernel<<<min(256, (batch + 255) / 256), 256, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
   const int blocks = (batch + a.gpb - 1) / a.gpb;
-  const int rows_pad = (a.gpb * N + 15) & ~15;
-  const size_t lds = ((size_t)rows_pad * LDH + (size_t)NWAVE * 16 * LDH) * sizeof(float);
-  const int ntiles = rows_pad / 16;
+  const size_t lds = lds_bytes(N, a.gpb, false);
+  const int ntiles = ((a.gpb * N + 15) & ~15) / 16;
+#define ECO_LAUNCH_FWD(MT, SV)                                                                                  \
+  do {                                                                                                         \
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<MT, SV>,                                        \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                          \
+    mpnn_forward_kernel<MT, SV><<<blocks, TPB, lds, st>>>(a);                                                  \
+  } while (0)
   if (ntiles <= 4 * NWAVE) {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_forward_kernel<4><<<blocks, TPB, lds, st>>>(a);
+    if (saved) ECO_LAUNCH_FWD(4, true); else ECO_LAUNCH_FWD(4, false);
   } else {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_forward_kernel<8><<<blocks, TPB, lds, st>>>(a);
+    if (saved) ECO_LAUNCH_FWD(8, true); else ECO_LAUNCH_FWD(8, false);
   }
+#undef ECO_LAUNCH_FWD
   return check_launch("mpnn_forward");
+}
+
+size_t eco::mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch) {
+  if (n_spins < 1 || batch < 1) return 0;
+  const int gpb = graphs_per_block(n_spins);
+  const size_t nblk = (batch + gpb - 1) / gpb;
+  return ((size_t)GR_NODE_TENSORS * n_spins * batch * 64 + 3 * (size_t)batch * 64 + (((size_t)batch + 63) & ~63ull) +
+          nblk * 64) * sizeof(float);
+}
+
+int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
+                              const int32_t* graph_ids, int32_t batch, const float* obs_x, const void* saved,
+                              const float* dq, void* gradws, hipStream_t st) {
+  MpnnArgs a;
+  int rc = prepare(a, packed, n_obs_in, gs, graph_ids, batch, obs_x, ECO_NORM_PER_CALL);
+  if (rc) return rc;
+  if (!saved || !dq || !gradws) return fail(ECO_ERR_ARG, "null saved/dq/workspace");
+  a.sv = (float*)saved;
+  a.dq = dq;
+  a.gr = (float*)gradws;
+  const int blocks = (batch + a.gpb - 1) / a.gpb;
+  const size_t lds = lds_bytes(a.N, a.gpb, true);
+  const int ntiles = ((a.gpb * a.N + 15) & ~15) / 16;
+  if (ntiles <= 4 * NWAVE) {
+    (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    mpnn_backward_kernel<4><<<blocks, TPB, lds, st>>>(a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    mpnn_backward_kernel<8><<<blocks, TPB, lds, st>>>(a);
+  }
+  return check_launch("mpnn_backward");
 }

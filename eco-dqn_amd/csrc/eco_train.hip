@@ -1,0 +1,326 @@
+// DQN training hot path on gfx950 (src/agents/dqn/dqn.py:403-451, dqn/utils.py:28-83):
+// device replay ring, double-DQN TD target + MSE gradient, MPNN weight gradients
+// (split-K reductions over every node of the minibatch on v_mfma_f32_32x32x2_f32,
+// per-wave partial slabs reduced in a fixed order -> bitwise reproducible), Adam.
+#include <cmath>
+
+#include "eco_mpnn.h"
+
+namespace eco {
+
+// ------------------------------------------------------------ weight grads ----
+// dW[o][i] = sum_r dY[r][o] * X[r][i]  with X = [X1 (K1 cols) | X2 (K2 cols)]
+struct WJob {
+  const float* dY;   // [R][64]
+  const float* X1;
+  const float* X2;
+  int ld1, K1, ld2, K2;
+  int R;
+  int nO;            // rows of dW (64, or 63 for the edge-embedding Wx)
+  int out_off;       // flat offset of dW[0][0]
+  int out_ld;        // row stride in the flat buffer
+  int out_col0;      // first column in the flat buffer
+};
+constexpr int MAX_JOBS = 10;
+constexpr int WG_PER_JOB = 64;
+constexpr int SLABS_PER_JOB = WG_PER_JOB * NWAVE;
+constexpr int SLAB = 64 * 128;
+
+struct WJobs {
+  WJob j[MAX_JOBS];
+  int n;
+};
+
+__global__ __launch_bounds__(TPB) void wgrad_kernel(WJobs jobs, float* slabs) {
+  const WJob& J = jobs.j[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int jj = lane & 31, h = lane >> 5;
+  const int K = J.K1 + J.K2;
+  const int chunk = ((J.R + WG_PER_JOB - 1) / WG_PER_JOB + 7) & ~7;
+  const int r0 = blockIdx.x * chunk;
+  const int r1 = min(J.R, r0 + chunk);
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[ot][it][k] = 0.f;
+  for (int rp = r0 + 2 * w; rp < r1; rp += 2 * NWAVE) {
+    const int r = rp + h;
+    const bool valid = r < r1;
+    const float a0 = valid ? J.dY[(size_t)r * 64 + jj] : 0.f;
+    const float a1 = valid ? J.dY[(size_t)r * 64 + 32 + jj] : 0.f;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      if (32 * it < K) {
+        const int col = 32 * it + jj;
+        float b = 0.f;
+        if (valid && col < K) b = col < J.K1 ? J.X1[(size_t)r * J.ld1 + col] : J.X2[(size_t)r * J.ld2 + col - J.K1];
+        acc[0][it] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[0][it], 0, 0, 0);
+        acc[1][it] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[1][it], 0, 0, 0);
+      }
+    }
+  }
+  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x * NWAVE + w) * SLAB;
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      if (32 * it < K) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
+          slab[o * 128 + 32 * it + jj] = acc[ot][it][k];
+        }
+      }
+    }
+}
+
+// fixed-order sum of the slabs of every job into the flat gradient
+__global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad) {
+  const WJob& J = jobs.j[blockIdx.y];
+  const int K = J.K1 + J.K2;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int o = idx / 128, i = idx % 128;
+  if (o >= J.nO || i >= K) return;
+  const float* s = slabs + (size_t)blockIdx.y * SLABS_PER_JOB * SLAB + o * 128 + i;
+  float acc = 0.f;
+  for (int k = 0; k < SLABS_PER_JOB; ++k) acc += s[(size_t)k * SLAB];
+  grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
+}
+
+// column sums in fixed order: out[c] = sum_r X[r][c]
+__global__ void colsum_kernel(const float* X, int R, int ld, int C, float* out, int out_stride) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.f;
+  for (int r = 0; r < R; ++r) acc += X[(size_t)r * ld + c];
+  out[(size_t)c * out_stride] = acc;
+}
+
+// ---------------------------------------------------------------------- TD ----
+// dqn.py:403-440 for a reversible env: q_t = target(s')[argmax online(s')] (double DQN),
+// td = r + (1 - done) * gamma * q_t, loss = mean((q(s,a) - td)^2), dq = dloss/dq.
+__global__ void td_kernel(const float* q_s, const float* q_tn, const int32_t* a_star, const int32_t* actions,
+                          const float* rewards, const float* dones, int B, int N, float gamma, int clip,
+                          float* dq, float* sqerr) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float qt = q_tn[(size_t)b * N + a_star[b]];
+  if (clip && qt < 0.f) qt = 0.f;  // clip_Q_targets (dqn.py:431-432)
+  const float td = rewards[b] + (1.f - dones[b]) * gamma * qt;
+  const int a = actions[b];
+  const float q = q_s[(size_t)b * N + a];
+  const float diff = q - td;
+  dq[(size_t)b * N + a] = 2.f * diff / (float)B;  // mse_loss(reduction='mean') backward
+  sqerr[b] = diff * diff;
+}
+
+__global__ void mean_kernel(const float* v, int n, float* out) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) acc += v[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0] / (float)n;
+}
+
+// -------------------------------------------------------------------- Adam ----
+// torch.optim.Adam (amsgrad=False): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps)      (dqn.py:212, :443-449)
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, int n, float b1, float b2, float step_size,
+                            float bc2_sqrt, float eps, float wd, float gscale) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = gscale == 1.f ? g[i] : g[i] * gscale;
+  if (wd != 0.f) gi = fmaf(wd, p[i], gi);
+  const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] - step_size * (mi / denom);
+}
+
+// ------------------------------------------------------------------ replay ----
+// ReplayBuffer (dqn/utils.py:28-83) as a device ring of compact transitions:
+// node features of s and s' ([N][8] fp32), graph id, action, reward, done.
+__global__ void replay_push_kernel(eco_replay rb, int pos, int B, const float* xs, const float* xn,
+                                   const int32_t* gids, const int32_t* actions, const double* rewards,
+                                   const uint8_t* dones) {
+  const int b = blockIdx.y;
+  if (b >= B) return;
+  const int slot = (int)(((long long)pos + b) % rb.capacity);
+  const int per = rb.n_spins * 8 / 4;  // float4s per state
+  const float4* s4 = reinterpret_cast<const float4*>(xs + (size_t)b * rb.n_spins * 8);
+  const float4* n4 = reinterpret_cast<const float4*>(xn + (size_t)b * rb.n_spins * 8);
+  float4* ds = reinterpret_cast<float4*>(rb.xs + (size_t)slot * rb.n_spins * 8);
+  float4* dn = reinterpret_cast<float4*>(rb.xn + (size_t)slot * rb.n_spins * 8);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per; i += gridDim.x * blockDim.x) {
+    ds[i] = s4[i];
+    dn[i] = n4[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rb.gid[slot] = gids[b];
+    rb.act[slot] = actions[b];
+    rb.rew[slot] = (float)rewards[b];  // torch.as_tensor([reward], dtype=torch.float) (dqn.py:299)
+    rb.done[slot] = dones[b] ? 1.f : 0.f;
+  }
+}
+
+// Feistel bijection on [0, 2^bits) with cycle walking into [0, n): distinct indices,
+// i.e. sampling WITHOUT replacement like random.sample (dqn/utils.py:53).
+__device__ __forceinline__ uint32_t feistel(uint32_t x, int half, uint64_t key) {
+  const uint32_t mask = (1u << half) - 1u;
+  uint32_t L = x >> half, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t F = (uint32_t)(rng3(key, (uint64_t)r, (uint64_t)R) & mask);
+    const uint32_t nL = R;
+    R = L ^ F;
+    L = nL;
+  }
+  return (L << half) | R;
+}
+
+__global__ void replay_sample_kernel(eco_replay rb, int size, int M, uint64_t key, float* xs, float* xn,
+                                     int32_t* gid, int32_t* act, float* rew, float* done) {
+  const int m = blockIdx.y;
+  if (m >= M) return;
+  int bits = 2;
+  while ((1 << bits) < size) ++bits;
+  if (bits & 1) ++bits;
+  const int half = bits / 2;
+  uint32_t x = (uint32_t)m;
+  do { x = feistel(x, half, key); } while (x >= (uint32_t)size);
+  const int slot = (int)x;
+  const int per = rb.n_spins * 8 / 4;
+  const float4* s4 = reinterpret_cast<const float4*>(rb.xs + (size_t)slot * rb.n_spins * 8);
+  const float4* n4 = reinterpret_cast<const float4*>(rb.xn + (size_t)slot * rb.n_spins * 8);
+  float4* ds = reinterpret_cast<float4*>(xs + (size_t)m * rb.n_spins * 8);
+  float4* dn = reinterpret_cast<float4*>(xn + (size_t)m * rb.n_spins * 8);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per; i += gridDim.x * blockDim.x) {
+    ds[i] = s4[i];
+    dn[i] = n4[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    gid[m] = rb.gid[slot];
+    act[m] = rb.act[slot];
+    rew[m] = rb.rew[slot];
+    done[m] = rb.done[slot];
+  }
+}
+
+static size_t slab_bytes() { return (size_t)MAX_JOBS * SLABS_PER_JOB * SLAB * sizeof(float); }
+
+}  // namespace eco
+
+using namespace eco;
+
+extern "C" size_t eco_mpnn_backward_workspace_bytes(int32_t n_spins, int32_t batch) {
+  const size_t g = mpnn_grad_ws_bytes(n_spins, batch);
+  if (!g) return 0;
+  return align_up(g, 256) + slab_bytes();
+}
+
+extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
+                                 const int32_t* graph_ids, int32_t batch, const float* obs_x, const void* saved,
+                                 const float* dq, float* grad, void* workspace, eco_stream_t stream) {
+  if (!grad || !workspace) return fail(ECO_ERR_ARG, "null grad/workspace");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = mpnn_backward_launch(packed, n_obs_in, gs, graph_ids, batch, obs_x, saved, dq, workspace, st);
+  if (rc) return rc;
+  const int N = gs->n_spins;
+  const size_t RT = (size_t)batch * N;
+  if (RT > (size_t)INT32_MAX / 64) return fail(ECO_ERR_ARG, "batch * n_spins too large");
+  const float* sv = (const float*)saved;
+  const float* gr = (const float*)workspace;
+  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
+  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
+  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
+  const float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
+  const float* DWRA = DP + (size_t)batch * 64;
+  const float* DWRB = DWRA + (size_t)batch * 64;
+  const float* DBR = DWRB + (size_t)batch * 64;
+  const float* DWA = DBR + (((size_t)batch + 63) & ~63ull);
+  const int gpb = graphs_per_block(N);
+  const int nblk = (batch + gpb - 1) / gpb;
+  float* slabs = (float*)((char*)workspace + align_up(mpnn_grad_ws_bytes(N, batch), 256));
+  const FlatOffsets fo = flat_offsets(n_obs_in);
+  WJobs J{};
+  int n = 0;
+  const int R = (int)RT;
+  for (int l = 0; l < 3; ++l) {
+    J.j[n++] = WJob{GR(GR_DUM0 + l), SV(SV_AGG0 + l), SV(SV_E), 64, 64, 64, 64, R, 64, fo.L + l * 16384, 128, 0};
+    J.j[n++] = WJob{GR(GR_DUU0 + l), SV(SV_H0 + l), SV(SV_M0 + l), 64, 64, 64, 64, R, 64, fo.L + l * 16384 + 8192,
+                    128, 0};
+  }
+  J.j[n++] = WJob{GR(GR_DUE), SV(SV_EAGG), nullptr, 64, 64, 0, 0, R, 64, fo.Wf, 64, 0};
+  J.j[n++] = WJob{GR(GR_DU0), obs_x, nullptr, 8, n_obs_in, 0, 0, R, 64, fo.W0, n_obs_in, 0};
+  J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, 8, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
+  J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
+  J.n = n;
+  wgrad_kernel<<<dim3(WG_PER_JOB, n), TPB, 0, st>>>(J, slabs);
+  wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
+  colsum_kernel<<<1, 64, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
+  colsum_kernel<<<1, 64, 0, st>>>(DWRB, batch, 64, 64, grad + fo.Wr + 64, 1);
+  colsum_kernel<<<1, 64, 0, st>>>(DBR, batch, 1, 1, grad + fo.Br, 1);
+  colsum_kernel<<<1, 64, 0, st>>>(DWA, nblk, 64, 63, grad + fo.We, 1 + n_obs_in);
+  return check_launch("mpnn_backward_wgrad");
+}
+
+extern "C" int eco_dqn_td(const float* q_s, const float* q_target_next, const int32_t* a_star,
+                          const int32_t* actions, const float* rewards, const float* dones, int32_t batch,
+                          int32_t n_spins, float gamma, int32_t clip_q_targets, float* dq, float* sqerr,
+                          float* loss, eco_stream_t stream) {
+  if (!q_s || !q_target_next || !a_star || !actions || !rewards || !dones || !dq || !sqerr || !loss)
+    return fail(ECO_ERR_ARG, "null argument");
+  if (batch < 1 || n_spins < 1) return fail(ECO_ERR_ARG, "bad batch/n_spins");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(dq, 0, sizeof(float) * (size_t)batch * n_spins, st) != hipSuccess)
+    return fail(ECO_ERR_HIP, "memset dq failed");
+  td_kernel<<<(batch + 255) / 256, 256, 0, st>>>(q_s, q_target_next, a_star, actions, rewards, dones, batch, n_spins,
+                                                 gamma, clip_q_targets, dq, sqerr);
+  mean_kernel<<<1, 256, 0, st>>>(sqerr, batch, loss);
+  return check_launch("dqn_td");
+}
+
+extern "C" int eco_adam(float* params, const float* grad, float* exp_avg, float* exp_avg_sq, int32_t n, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, double grad_scale, int64_t step,
+                        eco_stream_t stream) {
+  if (!params || !grad || !exp_avg || !exp_avg_sq || n < 1 || step < 1) return fail(ECO_ERR_ARG, "bad adam args");
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  adam_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(params, grad, exp_avg, exp_avg_sq, n, (float)beta1,
+                                                               (float)beta2, (float)(lr / bc1),
+                                                               (float)std::sqrt(bc2), (float)eps,
+                                                               (float)weight_decay, (float)grad_scale);
+  return check_launch("adam");
+}
+
+extern "C" int eco_replay_push(const eco_replay* rb, int32_t pos, int32_t batch, const float* xs, const float* xn,
+                               const int32_t* graph_ids, const int32_t* actions, const double* rewards,
+                               const uint8_t* dones, eco_stream_t stream) {
+  if (!rb || !xs || !xn || !graph_ids || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
+  if (batch < 1 || rb->capacity < 1 || pos < 0) return fail(ECO_ERR_ARG, "bad batch/capacity/pos");
+  replay_push_kernel<<<dim3(1, batch), 256, 0, (hipStream_t)stream>>>(*rb, pos, batch, xs, xn, graph_ids, actions,
+                                                                      rewards, dones);
+  return check_launch("replay_push");
+}
+
+extern "C" int eco_replay_sample(const eco_replay* rb, int32_t size, int32_t m, uint64_t seed, uint64_t counter,
+                                 float* xs, float* xn, int32_t* graph_ids, int32_t* actions, float* rewards,
+                                 float* dones, eco_stream_t stream) {
+  if (!rb || !xs || !xn || !graph_ids || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
+  if (size < m || m < 1 || size > rb->capacity)
+    return fail(ECO_ERR_ARG, "replay sample: need m <= size <= capacity (random.sample without replacement)");
+  replay_sample_kernel<<<dim3(1, m), 256, 0, (hipStream_t)stream>>>(*rb, size, m, rng3(seed, counter, 0x5A5A),
+                                                                    xs, xn, graph_ids, actions, rewards, dones);
+  return check_launch("replay_sample");
+}

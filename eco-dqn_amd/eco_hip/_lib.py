@@ -39,6 +39,12 @@ class GraphSet(ctypes.Structure):
                 ("max_deg", ctypes.c_void_p), ("meta", ctypes.c_void_p), ("valid", ctypes.c_void_p)]
 
 
+class Replay(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_int32), ("n_spins", ctypes.c_int32), ("xs", ctypes.c_void_p),
+                ("xn", ctypes.c_void_p), ("gid", ctypes.c_void_p), ("act", ctypes.c_void_p),
+                ("rew", ctypes.c_void_p), ("done", ctypes.c_void_p)]
+
+
 class ActConfig(ctypes.Structure):
     _fields_ = [("epsilon", ctypes.c_float), ("reversible", ctypes.c_int32), ("allowed_value", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("counter", ctypes.c_uint64)]
@@ -60,7 +66,16 @@ _SIG = {
     "eco_mpnn_pack": (ctypes.c_int, [_P, _I, _P, _P]),
     "eco_mpnn_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_mpnn_forward": (ctypes.c_int, [_P, _I, ctypes.POINTER(GraphSet), _P, _I, _P, _I, _P,
-                                        ctypes.POINTER(ActConfig), _P, _P, _P]),
+                                        ctypes.POINTER(ActConfig), _P, _P, _P, _P]),
+    "eco_mpnn_saved_bytes": (ctypes.c_size_t, [_I, _I]),
+    "eco_mpnn_backward_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
+    "eco_mpnn_backward": (ctypes.c_int, [_P, _I, ctypes.POINTER(GraphSet), _P, _I, _P, _P, _P, _P, _P, _P]),
+    "eco_dqn_td": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_float, _I, _P, _P, _P, _P]),
+    "eco_adam": (ctypes.c_int, [_P, _P, _P, _P, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int64, _P]),
+    "eco_replay_push": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "eco_replay_sample": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P,
+                                         _P, _P, _P, _P, _P]),
     "eco_last_error": (ctypes.c_char_p, []),
 }
 for _name, (_res, _args) in _SIG.items():

@@ -1,0 +1,295 @@
+"""Batched DQN agent (src/agents/dqn/dqn.py) on the HIP engine.
+
+Same constructor keywords and public methods as the reference DQN
+(`learn`, `train_step`, `act`, `predict`, `update_epsilon`, `update_lr`,
+`evaluate_agent`, `save`, `load`), but `envs` is a VecSpinSystem: every call
+advances B episodes.  Everything on the step path runs in libecohip:
+  act       -> MPNN forward with the fused epsilon-greedy argmax (dqn.py:453-465)
+  env.step  -> batched SpinSystem kernel (spinsystem.py:355-559)
+  replay    -> device ring push / distinct-index sample (dqn/utils.py:28-83)
+  train     -> online(s') argmax, target(s') gather, online(s) forward with saved
+               activations, TD + MSE gradient, MPNN backward, Adam (dqn.py:403-451)
+Schedules are per env-step as in the reference; a vector step advances the
+counter by B.  The replay ratio of the reference (minibatch_size/update_frequency
+samples per env-step, 64/32 = 2 in train_eco.py:136-137) is kept by running
+K = B*ratio/M gradient steps of minibatch M per vector step.  Multi-GPU: one
+process per GPU, episodes sharded, gradients summed over RCCL (torch.distributed)
+and averaged inside the Adam kernel; parameters stay bit-identical across ranks.
+"""
+import ctypes
+import math
+import os
+import random
+
+import numpy as np
+import torch
+
+from ... import _lib
+from .utils import ReplayBuffer, TestMetric, set_global_seed
+
+
+class DQN:
+    def __init__(self, envs, network, init_network_params=None, init_weight_std=None, double_dqn=True,
+                 update_target_frequency=10000, gamma=0.99, clip_Q_targets=False, replay_start_size=50000,
+                 replay_buffer_size=1000000, minibatch_size=32, update_frequency=1, update_learning_rate=True,
+                 initial_learning_rate=0, peak_learning_rate=1e-3, peak_learning_rate_step=10000,
+                 final_learning_rate=5e-5, final_learning_rate_step=200000, max_grad_norm=None, weight_decay=0,
+                 update_exploration=True, initial_exploration_rate=1, final_exploration_rate=0.1,
+                 final_exploration_step=1000000, adam_epsilon=1e-8, loss="mse", save_network_frequency=10000,
+                 network_save_path='network', evaluate=True, test_envs=None, test_episodes=20,
+                 test_frequency=10000, test_save_path='test_scores', test_metric=TestMetric.ENERGY_ERROR,
+                 logging=True, seed=None, train_minibatch=None, graph_pool_ids=None):
+        if isinstance(envs, (list, tuple)):
+            if len(envs) != 1:
+                raise NotImplementedError("pass one VecSpinSystem (it already holds B episodes)")
+            envs = envs[0]
+        if loss != "mse":
+            raise NotImplementedError("eco_hip implements the reference's training loss 'mse' (train_eco.py:148)")
+        if max_grad_norm is not None:
+            raise NotImplementedError("gradient clipping is not on the hot path (train_eco.py:138 uses None)")
+        self.env = envs
+        self.graphs = envs.graphs
+        self.device = envs.graphs.device
+        self.double_dqn = double_dqn
+        self.replay_start_size = replay_start_size
+        self.replay_buffer_size = replay_buffer_size
+        self.gamma = gamma
+        self.clip_Q_targets = clip_Q_targets
+        self.update_target_frequency = update_target_frequency
+        self.minibatch_size = minibatch_size
+        self.update_learning_rate = update_learning_rate
+        self.initial_learning_rate = initial_learning_rate
+        self.peak_learning_rate = peak_learning_rate
+        self.peak_learning_rate_step = peak_learning_rate_step
+        self.final_learning_rate = final_learning_rate
+        self.final_learning_rate_step = final_learning_rate_step
+        self.weight_decay = weight_decay
+        self.update_frequency = update_frequency
+        self.update_exploration = update_exploration
+        self.initial_exploration_rate = initial_exploration_rate
+        self.epsilon = initial_exploration_rate
+        self.final_exploration_rate = final_exploration_rate
+        self.final_exploration_step = final_exploration_step
+        self.adam_epsilon = adam_epsilon
+        self.lr = initial_learning_rate
+        self.logging = logging
+        self.seed = random.randint(0, 10 ** 6) if seed is None else seed
+        set_global_seed(self.seed)
+        self.acting_in_reversible_spin_env = envs.reversible_spins
+        self.allowed_value = envs.allowed_action_value()
+
+        self.network = network()
+        self.target_network = network()
+        if init_network_params is not None:
+            self.load(init_network_params)
+        elif init_weight_std is not None:
+            self.network.init_normal_(init_weight_std, generator=torch.Generator().manual_seed(self.seed))
+        self.target_network.load_state_dict(self.network.state_dict())
+        n = self.network.flat.numel()
+        self.grad = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.exp_avg = torch.zeros_like(self.grad)
+        self.exp_avg_sq = torch.zeros_like(self.grad)
+        self.adam_step = 0
+        self.grad_steps = 0
+
+        self.B = envs.n_envs
+        self.N = envs.n_spins
+        self.M = int(train_minibatch or minibatch_size)
+        self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed)
+        self.replay_ratio = minibatch_size / float(update_frequency)
+        # reference: one target sync per update_target_frequency env-steps = that many
+        # env-steps' worth of replayed samples
+        self.target_sync_samples = update_target_frequency * self.replay_ratio
+        self._samples_since_sync = 0.0
+        self.graph_pool_ids = (np.arange(self.graphs.n_graphs) if graph_pool_ids is None
+                               else np.asarray(graph_pool_ids))
+        self._rng = np.random.default_rng(self.seed)
+
+        self.evaluate = evaluate
+        self.test_envs = test_envs
+        self.test_episodes = int(test_episodes)
+        self.test_frequency = test_frequency
+        self.test_save_path = test_save_path
+        self.test_metric = test_metric
+        self.save_network_frequency = save_network_frequency
+        self.network_save_path = network_save_path
+
+        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        self.world = torch.distributed.get_world_size() if self.dist else 1
+        self._act_counter = 0
+        self._alloc_train_buffers(self.M)
+
+    # ---------------------------------------------------------------- buffers
+    def _alloc_train_buffers(self, m):
+        dev = self.device
+        self.q_s = torch.empty(m, self.N, device=dev)
+        self.q_tn = torch.empty(m, self.N, device=dev)
+        self.a_star = torch.empty(m, dtype=torch.int32, device=dev)
+        self.dq = torch.empty(m, self.N, device=dev)
+        self.sqerr = torch.empty(m, device=dev)
+        self.loss_dev = torch.zeros(1, device=dev)
+        self.saved = torch.empty(self.network.saved_bytes(self.N, m), dtype=torch.uint8, device=dev)
+        self.bw_ws = torch.empty(_lib.lib.eco_mpnn_backward_workspace_bytes(self.N, m), dtype=torch.uint8,
+                                 device=dev)
+        self._train_m = m
+        self._actions = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self._obs = [self.env.obs_x, torch.zeros_like(self.env.obs_x)]
+
+    # -------------------------------------------------------------- schedules
+    def update_epsilon(self, timestep):
+        """dqn.py:467-471"""
+        eps = self.initial_exploration_rate - (self.initial_exploration_rate - self.final_exploration_rate) * (
+            timestep / self.final_exploration_step)
+        self.epsilon = max(eps, self.final_exploration_rate)
+
+    def update_lr(self, timestep):
+        """dqn.py:473-488"""
+        if timestep <= self.peak_learning_rate_step:
+            lr = self.initial_learning_rate - (self.initial_learning_rate - self.peak_learning_rate) * (
+                timestep / self.peak_learning_rate_step)
+        elif timestep <= self.final_learning_rate_step:
+            lr = self.peak_learning_rate - (self.peak_learning_rate - self.final_learning_rate) * (
+                (timestep - self.peak_learning_rate_step) /
+                (self.final_learning_rate_step - self.peak_learning_rate_step))
+        else:
+            lr = None
+        if lr is not None:
+            self.lr = lr
+
+    # ------------------------------------------------------------------- act
+    def _act_config(self, epsilon):
+        self._act_counter += 1
+        return _lib.ActConfig(float(epsilon), int(self.acting_in_reversible_spin_env), float(self.allowed_value),
+                              self.seed, self._act_counter)
+
+    def act(self, obs_x, graph_ids, is_training_ready=True, actions_out=None):
+        """dqn.py:453-465 for every episode: epsilon-greedy over the MPNN (B=1 norm semantics, :282)."""
+        eps = self.epsilon if is_training_ready else 1.0
+        out = actions_out if actions_out is not None else torch.empty(obs_x.shape[0], dtype=torch.int32,
+                                                                       device=self.device)
+        self.network.forward_graphs(obs_x, self.graphs, graph_ids, norm_scope=_lib.ECO_NORM_PER_GRAPH,
+                                    act=self._act_config(eps), actions_out=out)
+        return out
+
+    @torch.no_grad()
+    def predict(self, obs_x, graph_ids, graphs=None, norm_scope=_lib.ECO_NORM_PER_CALL):
+        """dqn.py:490-512: greedy actions (allowed vertices only for irreversible envs)."""
+        out = torch.empty(obs_x.shape[0], dtype=torch.int32, device=self.device)
+        self.network.forward_graphs(obs_x, graphs or self.graphs, graph_ids, norm_scope=norm_scope,
+                                    act=self._act_config(0.0), actions_out=out)
+        return out
+
+    # ----------------------------------------------------------------- train
+    def train_step(self, transitions, sync_loss=True):
+        """dqn.py:403-451.  transitions = (states_x, actions, rewards, states_next_x, dones, graph_ids)
+        as returned by ReplayBuffer.sample.  Returns the loss (float if sync_loss else device tensor)."""
+        xs, act, rew, xn, done, gid = transitions
+        m = xs.shape[0]
+        if m != self._train_m:
+            self._alloc_train_buffers(m)
+        net, tgt = self.network, self.target_network
+        greedy = _lib.ActConfig(0.0, int(self.acting_in_reversible_spin_env), float(self.allowed_value), 0, 0)
+        if self.double_dqn:
+            # greedy_actions = network(s').argmax (masked for irreversible envs), q_t = target(s')[a*]
+            net.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, act=greedy,
+                               actions_out=self.a_star)
+            tgt.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_tn)
+        else:
+            tgt.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_tn,
+                               act=greedy, actions_out=self.a_star)
+        net.forward_graphs(xs, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_s,
+                           saved=self.saved)
+        _lib.check(_lib.lib.eco_dqn_td(_lib.ptr(self.q_s), _lib.ptr(self.q_tn), _lib.ptr(self.a_star),
+                                       _lib.ptr(act), _lib.ptr(rew), _lib.ptr(done), m, self.N,
+                                       ctypes.c_float(self.gamma), int(bool(self.clip_Q_targets)), _lib.ptr(self.dq),
+                                       _lib.ptr(self.sqerr), _lib.ptr(self.loss_dev), _lib.stream_ptr()))
+        net.backward_graphs(xs, self.graphs, gid, self.saved, self.dq, self.grad, workspace=self.bw_ws)
+        scale = 1.0
+        if self.dist and self.world > 1:
+            torch.distributed.all_reduce(self.grad)  # RCCL sum over xGMI: 233.7 KB per step
+            scale = 1.0 / self.world
+        self.adam_step += 1
+        _lib.check(_lib.lib.eco_adam(_lib.ptr(net.flat), _lib.ptr(self.grad), _lib.ptr(self.exp_avg),
+                                     _lib.ptr(self.exp_avg_sq), net.flat.numel(), self.lr, 0.9, 0.999,
+                                     self.adam_epsilon, float(self.weight_decay), scale, self.adam_step,
+                                     _lib.stream_ptr()))
+        net.repack()
+        self.grad_steps += 1
+        self._samples_since_sync += m
+        return self.loss_dev.item() if sync_loss else self.loss_dev
+
+    def sync_target(self):
+        """dqn.py:346-347: target <- online."""
+        self.target_network.flat.copy_(self.network.flat)
+
+    def _new_graph_ids(self, n):
+        return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
+
+    def vector_step(self, is_training_ready):
+        """One act -> env.step -> replay.add over all B episodes; returns the new obs buffer."""
+        x = self.env.obs_x
+        nxt = self._obs[1] if x.data_ptr() == self._obs[0].data_ptr() else self._obs[0]
+        self.act(x, self.env.graph_ids, is_training_ready, actions_out=self._actions)
+        _, rew, done = self.env.step(self._actions, obs_out=nxt)
+        self.replay_buffer.add_batch(x, nxt, self.env.graph_ids, self._actions, rew, done)
+        return nxt
+
+    def learn(self, timesteps, verbose=False, on_vector_step=None):
+        """dqn.py:256-395 with B episodes per vector step (timesteps counts env-steps)."""
+        B, T = self.B, self.env.max_steps
+        self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed)
+        steps_in_episode = 0
+        is_training_ready = False
+        timestep = 0
+        losses = []
+        k_per_vec = max(1, int(round(B * self.replay_ratio / self.M)))
+        while timestep < timesteps:
+            if not is_training_ready and len(self.replay_buffer) >= max(self.replay_start_size, self.M):
+                is_training_ready = True
+            self.vector_step(is_training_ready)
+            timestep += B
+            steps_in_episode += 1
+            if self.update_exploration:
+                self.update_epsilon(timestep)
+            if self.update_learning_rate:
+                self.update_lr(timestep)
+            if steps_in_episode == T:  # every episode shares T and started together
+                self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed + timestep)
+                steps_in_episode = 0
+            if is_training_ready:
+                for _ in range(k_per_vec):
+                    loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False)
+                    if self._samples_since_sync >= self.target_sync_samples:
+                        self.sync_target()
+                        self._samples_since_sync = 0.0
+                losses.append((timestep, loss))
+            if on_vector_step is not None:
+                on_vector_step(timestep)
+        return [(t, float(l.item())) for t, l in losses[-100:]]
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate_agent(self, test_env=None):
+        """dqn.py:514-602 with TestMetric.BEST: greedy rollouts of every test episode to the end;
+        returns (mean best score, mean best solution)."""
+        env = test_env or self.test_envs
+        env.reset(graph_ids=np.arange(env.n_envs) % env.graphs.n_graphs, seed=self.seed)
+        gids = env.graph_ids
+        acts = torch.empty(env.n_envs, dtype=torch.int32, device=self.device)
+        for _ in range(env.max_steps):
+            self.network.forward_graphs(env.obs_x, env.graphs, gids, norm_scope=_lib.ECO_NORM_PER_CALL,
+                                        act=self._act_config(0.0), actions_out=acts)
+            env.step(acts)
+        st = env.read()
+        return float(st["best_score"].mean()), float(st["best_solution"].mean())
+
+    # ------------------------------------------------------------ checkpoint
+    def save(self, path='network.pth'):
+        """dqn.py:604-607: torch.save(state_dict) -- loadable by the reference MPNN."""
+        if os.path.splitext(path)[-1] == '':
+            path = path + '.pth'
+        torch.save({k: v.detach().cpu().clone() for k, v in self.network.state_dict().items()}, path)
+
+    def load(self, path):
+        """dqn.py:609-610 (weights_only: state_dicts are plain tensors)."""
+        self.network.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))

@@ -90,7 +90,7 @@ class VecSpinSystem:
     def _s(self):
         return _lib.stream_ptr(self.stream)
 
-    def reset(self, graph_ids=None, spins=None, mask=None, seed=0):
+    def reset(self, graph_ids=None, spins=None, mask=None, seed=0, obs_out=None):
         if graph_ids is not None:
             gi = torch.as_tensor(graph_ids, dtype=torch.int32, device=self.graphs.device)
             if mask is None:
@@ -104,6 +104,8 @@ class VecSpinSystem:
         mk = None
         if mask is not None:
             mk = torch.as_tensor(mask, dtype=torch.uint8, device=self.graphs.device).contiguous()
+        if obs_out is not None:
+            self.obs_x = obs_out
         _lib.check(_lib.lib.eco_env_reset(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
                                           _lib.ptr(self.state), self.n_envs, _lib.ptr(self.graph_ids),
                                           _lib.ptr(sp), _lib.ptr(mk), ctypes.c_uint64(seed),
@@ -114,12 +116,17 @@ class VecSpinSystem:
             self.dones[mk.bool()] = 0
         return self.obs_x
 
-    def step(self, actions):
+    def step(self, actions, obs_out=None):
+        """Advance every episode by its action.  obs_out: optional [B, N, 8] buffer that
+        receives the new features (self.obs_x is then left untouched, so a caller can
+        keep s and s' without a copy); it becomes self.obs_x afterwards."""
         a = actions if actions.dtype == torch.int32 else actions.to(torch.int32)
+        out = self.obs_x if obs_out is None else obs_out
         _lib.check(_lib.lib.eco_env_step(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
                                          _lib.ptr(self.state), self.n_envs, _lib.ptr(a.contiguous()),
-                                         _lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(self.obs_x),
+                                         _lib.ptr(self.rewards), _lib.ptr(self.dones), _lib.ptr(out),
                                          _lib.ptr(self.obs_f64), self._s()))
+        self.obs_x = out
         return self.obs_x, self.rewards, self.dones
 
     def check_errors(self):

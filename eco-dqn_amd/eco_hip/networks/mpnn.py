@@ -110,9 +110,10 @@ class MPNN(torch.nn.Module):
 
     # ---- fast path: graphs resident in a GraphStore ----
     def forward_graphs(self, obs_x, graphs, graph_ids, norm_scope=_lib.ECO_NORM_PER_GRAPH, q_out=None,
-                       act=None, actions_out=None, stream=None):
+                       act=None, actions_out=None, saved=None, stream=None):
         """Q [B, N] for node features obs_x [B, N, 8] on graphs graph_ids [B] of `graphs`.
-        act: optional ActConfig -> fused epsilon-greedy actions written to actions_out [B] int32."""
+        act: optional ActConfig -> fused epsilon-greedy actions written to actions_out [B] int32.
+        saved: optional buffer (saved_bytes) that receives the activations for backward()."""
         B, N = obs_x.shape[0], obs_x.shape[1]
         self._ensure_packed(stream)
         if q_out is None and act is None:
@@ -121,8 +122,26 @@ class MPNN(torch.nn.Module):
         _lib.check(_lib.lib.eco_mpnn_forward(
             _lib.ptr(self.packed), self.n_obs_in, ctypes.byref(graphs.gs), _lib.ptr(gids.contiguous()), B,
             _lib.ptr(obs_x), norm_scope, _lib.ptr(q_out), ctypes.byref(act) if act is not None else None,
-            _lib.ptr(actions_out), _lib.ptr(self._workspace(N, B)), _lib.stream_ptr(stream)))
+            _lib.ptr(actions_out), _lib.ptr(saved), _lib.ptr(self._workspace(N, B)), _lib.stream_ptr(stream)))
         return q_out
+
+    @staticmethod
+    def saved_bytes(n_spins, batch):
+        return _lib.lib.eco_mpnn_saved_bytes(n_spins, batch)
+
+    def backward_graphs(self, obs_x, graphs, graph_ids, saved, dq, grad_out, workspace=None, stream=None):
+        """loss.backward(): grad_out[flat] = dLoss/dparams for dq = dLoss/dQ [B, N] of the forward that
+        filled `saved` (forward_graphs(..., norm_scope=ECO_NORM_PER_CALL, saved=...))."""
+        B, N = obs_x.shape[0], obs_x.shape[1]
+        need = _lib.lib.eco_mpnn_backward_workspace_bytes(N, B)
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty(need, dtype=torch.uint8, device=obs_x.device)
+        gids = graph_ids if graph_ids.dtype == torch.int32 else graph_ids.to(torch.int32)
+        _lib.check(_lib.lib.eco_mpnn_backward(
+            _lib.ptr(self.packed), self.n_obs_in, ctypes.byref(graphs.gs), _lib.ptr(gids.contiguous()), B,
+            _lib.ptr(obs_x), _lib.ptr(saved), _lib.ptr(dq), _lib.ptr(grad_out), _lib.ptr(workspace),
+            _lib.stream_ptr(stream)))
+        return grad_out
 
     # ---- reference-format forward (drop-in for mpnn.py:40-77) ----
     def forward(self, obs):

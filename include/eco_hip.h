@@ -159,14 +159,67 @@ typedef struct {
 } eco_act_config;
 
 size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch);
+/* Bytes of the activations a training forward saves for eco_mpnn_backward. */
+size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch);
 
 /* MPNN.forward (mpnn.py:40-77) on B graphs at once.
  * obs_x[B][N][8]: node features; adjacency = graphs graph_ids[B] of `gs`.
  * q[B][N] fp32 (may be NULL when only actions are wanted).
- * act / actions[B]: optional fused epsilon-greedy action selection. */
+ * act / actions[B]: optional fused epsilon-greedy action selection.
+ * saved: NULL for inference; for the training forward of train_step (dqn.py:437)
+ * a buffer of eco_mpnn_saved_bytes that receives the activations. */
 int eco_mpnn_forward(const float *packed, int32_t n_obs_in, const eco_graph_set *gs, const int32_t *graph_ids,
                      int32_t batch, const float *obs_x, int32_t norm_scope, float *q, const eco_act_config *act,
-                     int32_t *actions, void *workspace, eco_stream_t stream);
+                     int32_t *actions, void *saved, void *workspace, eco_stream_t stream);
+
+/* ---- DQN train step (dqn.py:403-451) ---- */
+
+size_t eco_mpnn_backward_workspace_bytes(int32_t n_spins, int32_t batch);
+/* loss.backward() through the MPNN: grad[flat, state_dict order] = dLoss/dparams
+ * for dq[B][N] = dLoss/dQ of the forward that filled `saved` (norm scope per call).
+ * grad is overwritten (zero_grad + backward).  Reductions are in a fixed order:
+ * results are bitwise reproducible run to run. */
+int eco_mpnn_backward(const float *packed, int32_t n_obs_in, const eco_graph_set *gs, const int32_t *graph_ids,
+                      int32_t batch, const float *obs_x, const void *saved, const float *dq, float *grad,
+                      void *workspace, eco_stream_t stream);
+
+/* Double-DQN TD target and MSE gradient (dqn.py:409-440, reversible env):
+ * q_t = q_target_next[b][a_star[b]] (a_star = argmax of the online net on s'),
+ * td = r + (1 - done) * gamma * q_t; loss = mean((q_s[b][a_b] - td)^2);
+ * dq[B][N] = dloss/dq (zero except at a_b); sqerr[B] scratch; loss[1]. */
+int eco_dqn_td(const float *q_s, const float *q_target_next, const int32_t *a_star, const int32_t *actions,
+               const float *rewards, const float *dones, int32_t batch, int32_t n_spins, float gamma,
+               int32_t clip_q_targets, float *dq, float *sqerr, float *loss, eco_stream_t stream);
+
+/* torch.optim.Adam step (dqn.py:212, optimizer.step() :449) on a flat fp32 buffer.
+ * grad_scale multiplies the gradient first (1/world after a multi-GPU sum all-reduce). */
+int eco_adam(float *params, const float *grad, float *exp_avg, float *exp_avg_sq, int32_t n, double lr,
+             double beta1, double beta2, double eps, double weight_decay, double grad_scale, int64_t step,
+             eco_stream_t stream);
+
+/* ReplayBuffer (dqn/utils.py:28-83) as a device ring of compact transitions.  Buffers are
+ * caller-owned: xs/xn [capacity][N][8] fp32 node features of s and s'; graph id, action,
+ * reward (fp32, dqn.py:299), done (fp32). */
+typedef struct {
+  int32_t capacity;
+  int32_t n_spins;
+  float *xs;
+  float *xn;
+  int32_t *gid;
+  int32_t *act;
+  float *rew;
+  float *done;
+} eco_replay;
+
+/* ReplayBuffer.add for B transitions into slots (pos + b) % capacity. */
+int eco_replay_push(const eco_replay *rb, int32_t pos, int32_t batch, const float *xs, const float *xn,
+                    const int32_t *graph_ids, const int32_t *actions, const double *rewards, const uint8_t *dones,
+                    eco_stream_t stream);
+/* ReplayBuffer.sample: m DISTINCT uniform slots of the first `size` (random.sample,
+ * dqn/utils.py:53), keyed by (seed, counter); gathered into minibatch buffers. */
+int eco_replay_sample(const eco_replay *rb, int32_t size, int32_t m, uint64_t seed, uint64_t counter, float *xs,
+                      float *xn, int32_t *graph_ids, int32_t *actions, float *rewards, float *dones,
+                      eco_stream_t stream);
 
 /* Device-side errors (bad action, invalid graph, non-signed injected spins) are
  * recorded in a device word by the asynchronous kernels; this synchronises
