@@ -1,17 +1,24 @@
 #!/usr/bin/env python
 """Benchmark: env-steps/sec (batched episodes) on ER-200 MaxCut (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload rollout|train] [--envs B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload train|rollout] [--envs B] [--n N]
 
-One "step" = one vector step over B=8192 concurrent ER-200 episodes (each on its own
-graph): MPNN forward + fused epsilon-greedy act + env step, all on the GPU
-(workload "rollout"); "train" adds the DQN update (replay + TD + backward + Adam)
-once it is available.  value = B * K * world / max-over-ranks(time).  Episodes
-shard across ranks with no data-path collective (scaling "weak").
+Default workload = BASELINE.json configs[2]: ER_200spin, 8192 parallel episodes per
+GPU (each on its own graph), the FULL ECO-DQN train loop:
+  one step = one vector step of DQN.learn over all B episodes:
+     MPNN forward + fused eps-greedy act, batched env step, replay add,
+     then K = B * (64/32) / M gradient steps of minibatch M (replay ratio of
+     train_eco.py:136-137): replay sample, online(s') argmax, target(s') gather,
+     online(s) forward, TD + MSE grad, MPNN backward, Adam, target sync.
+  "rollout" = the act + env step part only.
+value = B * K * world / max-over-ranks(time): episodes shard across ranks; the
+train loop all-reduces gradients over RCCL (weak scaling, B fixed per GPU).
 
-Prints ONE JSON line on rank 0 with roofline (dominant kernel: mpnn_forward,
-MFMA-bound) and cpu_baseline (oracle = reference-cost numpy restatement of
-SpinSystem.step + torch-CPU MPNN forward, timed on this host on a bounded sample).
+Prints ONE JSON line on rank 0 with
+  roofline: dominant kernel measured live with HIP events (on the launch stream),
+            algorithmic FLOPs from SURVEY.md 8d: forward F = 1392*nnz + 107,648*N + 8,192
+            per graph, backward = 2F; peak = dense f32-input MFMA (157.3 TFLOP/s).
+  cpu_baseline: the oracle ('port') env + torch-CPU MPNN act loop on this host.
 """
 import argparse
 import json
@@ -29,44 +36,63 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
 
 
 def mpnn_flops(nnz, n):
-    """algorithmic forward FLOPs of one graph = 1392*nnz + 107,648*N + 8,192."""
+    """algorithmic forward FLOPs of one graph."""
     return 1392.0 * nnz + 107648.0 * n + 8192.0
 
 
-def cpu_baseline(n=200, seconds=12.0):
-    """Oracle (CPU 'port') env + MPNN forward, B=1 greedy act (dqn.py:282 path), ER-200."""
+def cpu_baseline(n=200, seconds=12.0, train=True):
+    """Oracle (CPU 'port'): SpinSystem.step restatement + torch-CPU MPNN forward, B=1
+    epsilon-greedy act (dqn.py:282 path); with train=True also one oracle train_step of
+    minibatch 64 every 32 env-steps (train_eco.py:136-137), i.e. the reference's learn loop."""
     sys.path.insert(0, REPO)
     from oracle import spinsystem_oracle as so
     from oracle import mpnn_oracle as mo
     from oracle import graphs as og
     rng = np.random.default_rng(0)
     w = mo.init_weights(torch.Generator().manual_seed(0), std=0.01)
+    adam = {"step": 0, "m": {}, "v": {}}
+    buf = []
     steps = 0
     t0 = time.perf_counter()
-    with torch.no_grad():
-        while time.perf_counter() - t0 < seconds:
-            J = og.er_graph(n, 0.15, rng)
-            env = so.SpinSystemOracle(J, 2 * n, basin_reward=1. / n)
-            obs = env.reset(rng=np.random.RandomState(int(rng.integers(1 << 31))))
-            done = False
-            while not done and time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < seconds:
+        J = og.er_graph(n, 0.15, rng)
+        env = so.SpinSystemOracle(J, 2 * n, basin_reward=1. / n)
+        obs = env.reset(rng=np.random.RandomState(int(rng.integers(1 << 31))))
+        done = False
+        while not done and time.perf_counter() - t0 < seconds:
+            with torch.no_grad():
                 q = mo.forward(w, torch.from_numpy(obs).float())
-                obs, _, done, _ = env.step(int(q.argmax()))
-                steps += 1
+            a = int(q.argmax()) if rng.random() >= 0.05 else int(rng.integers(n))
+            obs2, r, done, _ = env.step(a)
+            steps += 1
+            if train:
+                buf.append((obs, a, r, obs2, float(done)))
+                buf = buf[-2000:]
+                if steps % 32 == 0 and len(buf) >= 64:
+                    idx = rng.choice(len(buf), 64, replace=False)
+                    tr = [buf[i] for i in idx]
+                    w, _ = mo.train_step(w, adam, torch.from_numpy(np.array([t[0] for t in tr])).float(),
+                                         torch.tensor([[t[1]] for t in tr]), torch.tensor([[t[2]] for t in tr],
+                                                                                         dtype=torch.float32),
+                                         torch.from_numpy(np.array([t[3] for t in tr])).float(),
+                                         torch.tensor([[t[4]] for t in tr], dtype=torch.float32))
+            obs = obs2
     dt = time.perf_counter() - t0
+    what = "learn loop: act + env.step + train_step(64) every 32 steps" if train else "act + env.step"
     return dict(value=steps / dt, unit="env-steps/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"{steps} ER-200 env-steps (oracle SpinSystem.step + torch-CPU MPNN fwd, B=1 greedy), "
-                       f"{dt:.1f}s")
+                sample=f"{steps} ER-200 env-steps in {dt:.1f}s of the oracle {what} "
+                       f"(numpy SpinSystem restatement + torch-CPU MPNN, B=1)")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--n", type=int, default=200)
-    ap.add_argument("--workload", default="rollout", choices=["rollout"])
+    ap.add_argument("--minibatch", type=int, default=2048, help="M graphs per gradient step")
+    ap.add_argument("--workload", default="train", choices=["train", "rollout"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -78,70 +104,85 @@ def main():
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
 
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
                                     SpinBasis)
     from eco_hip.networks.mpnn import MPNN
-    from eco_hip._lib import ActConfig
+    from eco_hip.agents.dqn.dqn import DQN
 
     B, n = args.envs, args.n
     T = 2 * n
     seed = 1234 + rank
     store = GraphStore.random("ER", B, n, 0.15, seed=seed, device=dev)
     nnz = np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1)
-    flops_per_fwd = float(sum(mpnn_flops(z, n) for z in nnz))
+    gflops = np.array([mpnn_flops(z, n) for z in nnz])
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
                         spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
-    net = MPNN(device=dev)
-    net.init_normal_(0.01, generator=torch.Generator().manual_seed(seed))
-    gids = torch.arange(B, dtype=torch.int32, device=dev)
-    actions = torch.zeros(B, dtype=torch.int32, device=dev)
-    q = torch.empty(B, n, dtype=torch.float32, device=dev)
-    x = env.reset(graph_ids=gids, seed=seed)
-    counter = [0]
+    # experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377), batched
+    agent = DQN(env, lambda: MPNN(device=dev), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
+                replay_start_size=3000, replay_buffer_size=B * 16, gamma=0.95, update_target_frequency=4000,
+                update_learning_rate=False, initial_learning_rate=1e-4, peak_learning_rate=1e-4,
+                final_learning_rate=1e-4, update_frequency=32, minibatch_size=64, train_minibatch=args.minibatch,
+                initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
+                adam_epsilon=1e-8, seed=seed)
+    agent.start()
+    train = args.workload == "train"
 
-    def vec_step():
-        # epsilon from the C3 schedule mid-way (dqn.py:467-471): greedy with prob 1-eps
-        counter[0] += 1
-        act = ActConfig(0.05, 1, 0.0, seed, counter[0])
-        net.forward_graphs(x, store, gids, q_out=q, act=act, actions_out=actions)
-        env.step(actions)
-        if counter[0] % T == 0:  # all episodes finish together (same T): reset on new spins
-            env.reset(graph_ids=gids, seed=seed + counter[0])
+    def one_step():
+        if train:
+            agent.iteration()
+        else:
+            agent.vector_step(True)
 
-    for _ in range(args.warmup):
-        vec_step()
+    # warmup: fills the replay past replay_start_size, so every timed step trains
+    for _ in range(max(args.warmup, 1)):
+        one_step()
     torch.cuda.synchronize()
+    timers = []
+    agent.network.timer = timers
+    agent.target_network.timer = timers
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        counter[0] += 1
-        act = ActConfig(0.05, 1, 0.0, seed, counter[0])
-        ev[i][0].record()
-        net.forward_graphs(x, store, gids, q_out=q, act=act, actions_out=actions)
-        ev[i][1].record()
-        env.step(actions)
-        if counter[0] % T == 0:
-            env.reset(graph_ids=gids, seed=seed + counter[0])
+    for _ in range(args.steps):
+        one_step()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    agent.network.timer = None
+    agent.target_network.timer = None
     if dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = t.item()
-    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    achieved = flops_per_fwd / (fwd_ms * 1e-3) / 1e12
+
+    # per-kernel roofline from the live events: forward launches vs backward launches
+    kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}
+    mean_gf = float(gflops.mean())  # sampled minibatches draw from this pool: use its mean per graph
+    for e0, e1, b, _ in timers:
+        ms = e0.elapsed_time(e1)
+        fl = mean_gf * abs(b)
+        key = "mpnn_forward_kernel" if b > 0 else "mpnn_backward(+wgrad)"
+        kern[key][0] += ms
+        kern[key][1] += fl * (1 if b > 0 else 2)
+        kern[key][2] += 1
+    dom = max(kern, key=lambda k: kern[k][0])
+    ms, fl, cnt = kern[dom]
+    avg_ms = ms / max(cnt, 1)
+    achieved = fl / max(ms, 1e-9) / 1e9  # TFLOP/s
     value = B * args.steps * world / dt
     if rank == 0:
+        wl = ("ER_200spin x%d envs/GPU: full ECO-DQN train loop per vector step (act + env step + replay add "
+              "+ %d grad steps of M=%d: sample, double-DQN TD, MPNN fwd/bwd, Adam)"
+              % (B, agent._k_per_vec, args.minibatch)) if train else \
+             ("ER_200spin x%d envs/GPU: rollout only (MPNN fwd + eps-greedy act + env step + replay add)" % B)
         out = {
             "metric": "env-steps/sec (batched episodes) on ER-200 MaxCut",
             "value": value,
@@ -153,18 +194,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (MPNN, exact-f32 MFMA) / f64+int (env)",
-            "data": "synthetic: seeded ER(200, p=0.15) +-1 graphs, one per episode; random-init MPNN",
-            "config": {"workload": "ER_200spin x8192 envs/GPU: MPNN fwd + eps-greedy act + env step "
-                                   "(rollout half of configs[2]; DQN update not yet in the timed step)",
-                       "n_spins": n, "envs_per_gpu": B, "max_steps": T, "parallelism": f"episodes sharded dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "mpnn_forward_kernel", "achieved": achieved,
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": None, "fwd_ms": fwd_ms,
-                         "flops_per_launch": flops_per_fwd},
+            "dtype": "f32 (MPNN fwd/bwd on exact-f32 MFMA) / f64+int (env)",
+            "data": "synthetic: seeded ER(200, p=0.15) +-1 graphs, one per episode; random-init MPNN (std 0.01)",
+            "config": {"workload": wl, "n_spins": n, "envs_per_gpu": B, "max_steps": T,
+                       "train_minibatch": args.minibatch, "grad_steps_per_vector_step": agent._k_per_vec if train else 0,
+                       "replay_ratio": 2.0, "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "avg_launch_ms": avg_ms, "launches": cnt,
+                         "flops_per_launch": fl / max(cnt, 1)},
+            "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(n)
+            out["cpu_baseline"] = cpu_baseline(n, train=train)
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()

@@ -216,7 +216,7 @@ class DQN:
         net.repack()
         self.grad_steps += 1
         self._samples_since_sync += m
-        return self.loss_dev.item() if sync_loss else self.loss_dev
+        return self.loss_dev.item() if sync_loss else self.loss_dev.clone()
 
     def sync_target(self):
         """dqn.py:346-347: target <- online."""
@@ -234,37 +234,49 @@ class DQN:
         self.replay_buffer.add_batch(x, nxt, self.env.graph_ids, self._actions, rew, done)
         return nxt
 
+    def start(self):
+        """Reset every episode on fresh pool graphs (start of learn)."""
+        self.env.reset(graph_ids=self._new_graph_ids(self.B), seed=self.seed)
+        self._steps_in_episode = 0
+        self._timestep = 0
+        self._ready = False
+        self._k_per_vec = max(1, int(round(self.B * self.replay_ratio / self.M)))
+        self._last_loss = None
+
+    def iteration(self):
+        """One vector step of DQN.learn (dqn.py:273-347): act/step/add for all B episodes, reset
+        finished episodes, then K gradient steps (replay ratio preserved) with target syncs."""
+        B, T = self.B, self.env.max_steps
+        if not self._ready and len(self.replay_buffer) >= max(self.replay_start_size, self.M):
+            self._ready = True
+        self.vector_step(self._ready)
+        self._timestep += B
+        self._steps_in_episode += 1
+        if self.update_exploration:
+            self.update_epsilon(self._timestep)
+        if self.update_learning_rate:
+            self.update_lr(self._timestep)
+        if self._steps_in_episode == T:  # every episode shares T and started together
+            self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed + self._timestep)
+            self._steps_in_episode = 0
+        if self._ready:
+            for _ in range(self._k_per_vec):
+                self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False)
+                if self._samples_since_sync >= self.target_sync_samples:
+                    self.sync_target()
+                    self._samples_since_sync = 0.0
+        return self._last_loss
+
     def learn(self, timesteps, verbose=False, on_vector_step=None):
         """dqn.py:256-395 with B episodes per vector step (timesteps counts env-steps)."""
-        B, T = self.B, self.env.max_steps
-        self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed)
-        steps_in_episode = 0
-        is_training_ready = False
-        timestep = 0
+        self.start()
         losses = []
-        k_per_vec = max(1, int(round(B * self.replay_ratio / self.M)))
-        while timestep < timesteps:
-            if not is_training_ready and len(self.replay_buffer) >= max(self.replay_start_size, self.M):
-                is_training_ready = True
-            self.vector_step(is_training_ready)
-            timestep += B
-            steps_in_episode += 1
-            if self.update_exploration:
-                self.update_epsilon(timestep)
-            if self.update_learning_rate:
-                self.update_lr(timestep)
-            if steps_in_episode == T:  # every episode shares T and started together
-                self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed + timestep)
-                steps_in_episode = 0
-            if is_training_ready:
-                for _ in range(k_per_vec):
-                    loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False)
-                    if self._samples_since_sync >= self.target_sync_samples:
-                        self.sync_target()
-                        self._samples_since_sync = 0.0
-                losses.append((timestep, loss))
+        while self._timestep < timesteps:
+            loss = self.iteration()
+            if loss is not None:
+                losses.append((self._timestep, loss))
             if on_vector_step is not None:
-                on_vector_step(timestep)
+                on_vector_step(self._timestep)
         return [(t, float(l.item())) for t, l in losses[-100:]]
 
     # ------------------------------------------------------------------ eval

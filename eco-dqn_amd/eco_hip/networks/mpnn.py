@@ -61,6 +61,7 @@ class MPNN(torch.nn.Module):
         self.packed = torch.zeros(_lib.lib.eco_mpnn_packed_count(), dtype=torch.float32, device=dev)
         self._packed_version = -1
         self._ws = None
+        self.timer = None   # optional list: (start_event, end_event, batch, n_spins) per forward launch
 
     def _register_dotted(self, name, p):
         """Register `p` under its exact reference state_dict key (nested submodules)."""
@@ -119,10 +120,16 @@ class MPNN(torch.nn.Module):
         if q_out is None and act is None:
             q_out = torch.empty(B, N, dtype=torch.float32, device=obs_x.device)
         gids = graph_ids if graph_ids.dtype == torch.int32 else graph_ids.to(torch.int32)
+        if self.timer is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         _lib.check(_lib.lib.eco_mpnn_forward(
             _lib.ptr(self.packed), self.n_obs_in, ctypes.byref(graphs.gs), _lib.ptr(gids.contiguous()), B,
             _lib.ptr(obs_x), norm_scope, _lib.ptr(q_out), ctypes.byref(act) if act is not None else None,
             _lib.ptr(actions_out), _lib.ptr(saved), _lib.ptr(self._workspace(N, B)), _lib.stream_ptr(stream)))
+        if self.timer is not None:
+            ev[1].record()
+            self.timer.append((ev[0], ev[1], B, graph_ids))
         return q_out
 
     @staticmethod
@@ -137,10 +144,16 @@ class MPNN(torch.nn.Module):
         if workspace is None or workspace.numel() < need:
             workspace = torch.empty(need, dtype=torch.uint8, device=obs_x.device)
         gids = graph_ids if graph_ids.dtype == torch.int32 else graph_ids.to(torch.int32)
+        if self.timer is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         _lib.check(_lib.lib.eco_mpnn_backward(
             _lib.ptr(self.packed), self.n_obs_in, ctypes.byref(graphs.gs), _lib.ptr(gids.contiguous()), B,
             _lib.ptr(obs_x), _lib.ptr(saved), _lib.ptr(dq), _lib.ptr(grad_out), _lib.ptr(workspace),
             _lib.stream_ptr(stream)))
+        if self.timer is not None:
+            ev[1].record()
+            self.timer.append((ev[0], ev[1], -B, graph_ids))   # negative batch marks a backward launch
         return grad_out
 
     # ---- reference-format forward (drop-in for mpnn.py:40-77) ----
