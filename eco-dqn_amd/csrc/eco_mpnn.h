@@ -8,9 +8,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int MPNN_MAX_SPINS = 512;  // block of one graph must fit LDS (rows_pad * 272 B + scratch)
-constexpr int LDH = 68;              // LDS row stride (floats) of node-embedding tiles
-constexpr int NWAVE = 4;
-constexpr int TPB = 64 * NWAVE;
+constexpr int LDH = 68;              // LDS row stride (floats) of 64-wide tiles: 16 rows -> distinct bank quads
+constexpr int LDW = 132;             // LDS row stride of staged [64][128] weights (same property)
 
 // ---- packed parameter image (floats) ----
 constexpr int PK_W0 = 0;                     // [64][8]  node_init_embedding (cols >= n_obs zero)
@@ -50,7 +49,8 @@ enum { SV_H0 = 0, SV_H1, SV_H2, SV_H3, SV_E, SV_EAGG, SV_M0, SV_M1, SV_M2, SV_AG
 enum { GR_DUU0 = 0, GR_DUU1, GR_DUU2, GR_DUM0, GR_DUM1, GR_DUM2, GR_DUE, GR_DU0, GR_DZ, GR_DE, GR_DH,
        GR_NODE_TENSORS };  // then DP [B][64], DWRA [B][64], DWRB [B][64], DBR [B(pad 64)], DWA [nblocks][64]
 
-inline int graphs_per_block(int N) { return N >= 256 ? 1 : 256 / N; }
+// whole graphs per workgroup block: up to 208 rows (13 tiles) share the LDS-resident embeddings
+inline int graphs_per_block(int N) { return N >= 208 ? 1 : 208 / N; }
 
 size_t mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch);
 int mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_graph_set* gs, const int32_t* graph_ids,

@@ -78,18 +78,31 @@ struct MpnnArgs {
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
-// acc[nt] += A(16 rows x 16 k, one float4 per lane) * W[nt*16 + (l&15)][kbase + 4(l>>4) + 0..3]
-template <int NT>
-__device__ __forceinline__ void mm_chunk(f32x4 (&acc)[NT], float4 a, const float* __restrict__ W, int ldw, int kbase,
-                                         int lane) {
-  const float* wp = W + (lane & 15) * ldw + kbase + 4 * (lane >> 4);
+// acc[nt] += sum_c A_c * W[nt*16 + (l&15)][16c + 4(l>>4) + 0..3] over NC chunks of 16 k, with the
+// weight fragments of chunk c+1 loaded while chunk c's MFMAs run (one-chunk-ahead software
+// pipeline: without it every weight load is followed by s_waitcnt vmcnt(0)).
+template <int NT, int NC>
+__device__ __forceinline__ void mm_k(f32x4 (&acc)[NT], const float4 (&a)[NC], const float* __restrict__ W, int ldw,
+                                     int lane) {
+  const float* wp = W + (lane & 15) * ldw + 4 * (lane >> 4);
+  float4 b[2][NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const float4 b = *reinterpret_cast<const float4*>(wp + nt * 16 * ldw);
-    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[nt], 0, 0, 0);
-    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[nt], 0, 0, 0);
-    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[nt], 0, 0, 0);
-    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[nt], 0, 0, 0);
+  for (int nt = 0; nt < NT; ++nt) b[0][nt] = *reinterpret_cast<const float4*>(wp + nt * 16 * ldw);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + 1 < NC) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        b[(c + 1) & 1][nt] = *reinterpret_cast<const float4*>(wp + nt * 16 * ldw + 16 * (c + 1));
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float4 bb = b[c & 1][nt];
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].x, bb.x, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].y, bb.y, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].z, bb.z, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].w, bb.w, acc[nt], 0, 0, 0);
+    }
   }
 }
 
@@ -150,9 +163,24 @@ __device__ __forceinline__ void gather_rows(const NodeRef& n, const float* S, in
   }
 }
 
-template <int MAXT, bool SAVE>
-__global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
+// stage a rows x cols fp32 matrix (cols % 4 == 0) from global (row stride lds_) into LDS (row stride ldd)
+template <int NTHREADS>
+__device__ __forceinline__ void stage_rows(float* dst, int ldd, const float* __restrict__ src, int lds_, int rows,
+                                           int cols) {
+  const int per_row = cols >> 2;
+  for (int i = threadIdx.x; i < rows * per_row; i += NTHREADS) {
+    const int r = i / per_row, c = (i - r * per_row) * 4;
+    *reinterpret_cast<float4*>(dst + r * ldd + c) = *reinterpret_cast<const float4*>(src + r * lds_ + c);
+  }
+}
+
+// MAXT: max 16-node tiles per wave; NW: waves per workgroup; WLDS: stage each layer's weights in
+// LDS (one copy per workgroup, read as conflict-free ds_read_b128 B operands) instead of
+// streaming them from L2 in every wave.
+template <int MAXT, bool SAVE, int NW, bool WLDS>
+__global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NWAVE = NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int blk = blockIdx.x;
@@ -162,7 +190,9 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
   float* Hs = lds;                                  // [rows_pad][LDH]
-  float* Ms = lds + rows_pad * LDH + w * 16 * LDH;  // per-wave [16][LDH]
+  float* Wl = lds + rows_pad * LDH;                 // [2][64][LDW] staged weights (WLDS)
+  float* Ms = Wl + (WLDS ? 2 * 64 * LDW : 0) + w * 16 * LDH;  // per-wave [16][LDH]
+  if constexpr (WLDS) stage_rows<64 * NW>(Wl, LDH, a.P + PK_WF, 64, 64, 64);  // Wf, read after phase A's barrier
   const size_t R0 = (size_t)blk * a.gpb * N;        // first global row of the block
   const size_t RT = (size_t)a.B * N;                // rows of the call
   const float* P = a.P;
@@ -234,8 +264,8 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) mm_chunk<4>(d, acc[c], P + PK_WF, 64, 16 * c, lane);
+      if constexpr (WLDS) mm_k<4, 4>(d, acc, Wl, LDH, lane);
+      else mm_k<4, 4>(d, acc, P + PK_WF, 64, lane);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = t * 16 + 4 * s4 + rr;
@@ -271,6 +301,11 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
   for (int layer = 0; layer < 3; ++layer) {
     const float* Wm = P + PK_LAYER + layer * 16384;
     const float* Wu = Wm + 8192;
+    if constexpr (WLDS) {  // the previous readers of Wl finished at the last barrier
+      stage_rows<64 * NW>(Wl, LDW, Wm, 128, 64, 128);
+      stage_rows<64 * NW>(Wl + 64 * LDW, LDW, Wu, 128, 64, 128);
+      __syncthreads();
+    }
     f32x4 hn[MAXT][4];
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
@@ -278,6 +313,10 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
       if (t < ntiles) {
         const int r = t * 16 + (lane & 15);
         const NodeRef n = node_ref(a, blk, r, rows_valid);
+        // operand block of the message Linear: [agg (4 chunks), e (4 chunks)]; e is issued first
+        float4 am[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) am[4 + c] = n.valid ? f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
         // aggregation (A . h) / norm, in A-operand layout
         float4 agg[4];
 #pragma unroll
@@ -298,13 +337,9 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) mm_chunk<4>(d, agg[c], Wm, 128, 16 * c, lane);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float4 ev = zero4();
-          if (n.valid) ev = f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4);
-          mm_chunk<4>(d, ev, Wm, 128, 64 + 16 * c, lane);
-        }
+        for (int c = 0; c < 4; ++c) am[c] = agg[c];
+        if constexpr (WLDS) mm_k<4, 8>(d, am, Wl, LDW, lane);
+        else mm_k<4, 8>(d, am, Wm, 128, lane);
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int row = t * 16 + 4 * s4 + rr;
@@ -320,11 +355,14 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
         // h' = relu(Wu . [h, m])
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float4 au[8];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) mm_chunk<4>(hn[ti], f4(Hs + r * LDH + 16 * c + 4 * s4), Wu, 128, 16 * c, lane);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          mm_chunk<4>(hn[ti], f4(Ms + (lane & 15) * LDH + 16 * c + 4 * s4), Wu, 128, 64 + 16 * c, lane);
+        for (int c = 0; c < 4; ++c) {
+          au[c] = f4(Hs + r * LDH + 16 * c + 4 * s4);
+          au[4 + c] = f4(Ms + (lane & 15) * LDH + 16 * c + 4 * s4);
+        }
+        if constexpr (WLDS) mm_k<4, 8>(hn[ti], au, Wl + 64 * LDW, LDW, lane);
+        else mm_k<4, 8>(hn[ti], au, Wu, 128, lane);
         wave_lds_sync();
       }
     }
@@ -433,9 +471,10 @@ __global__ __launch_bounds__(TPB) void mpnn_forward_kernel(MpnnArgs a) {
 // forward saved in a.sv.  This kernel produces the activation gradients (the
 // pre-activation gradients dY of every Linear, stored [R][64]) and the small
 // per-graph / per-block partials; eco_train.hip reduces dW = sum_nodes dY^T X.
-template <int MAXT>
-__global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
+template <int MAXT, int NW, bool WLDS>
+__global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NWAVE = NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int blk = blockIdx.x;
@@ -445,8 +484,9 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
   float* G = lds;                                            // [rows_pad][LDH] gathered-gradient source
-  float* Ms = lds + rows_pad * LDH + w * 16 * LDH;           // per-wave transpose scratch
-  float* DMEAN = lds + rows_pad * LDH + NWAVE * 16 * LDH;    // [gpb][64]
+  float* Wl = lds + rows_pad * LDH;                          // [2][128][LDH] staged W^T (WLDS)
+  float* Ms = Wl + (WLDS ? 2 * 128 * LDH : 0) + w * 16 * LDH;  // per-wave transpose scratch
+  float* DMEAN = Wl + (WLDS ? 2 * 128 * LDH : 0) + NWAVE * 16 * LDH;  // [gpb][64]
   float* RED = DMEAN + a.gpb * 64;                           // [NWAVE][64] dwa partials
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
@@ -517,6 +557,11 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
   for (int layer = 2; layer >= 0; --layer) {
     const float* WmT = P + PK_LAYERT + layer * 16384;  // [128][64]
     const float* WuT = WmT + 8192;                      // [128][64]
+    if constexpr (WLDS) {  // previous readers of Wl finished at the last barrier
+      stage_rows<64 * NW>(Wl, LDH, WuT, 64, 128, 64);
+      stage_rows<64 * NW>(Wl + 128 * LDH, LDH, WmT, 64, 128, 64);
+      __syncthreads();
+    }
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
@@ -537,8 +582,8 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
         f32x4 d8[8];
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) mm_chunk<8>(d8, duu[c], WuT, 64, 16 * c, lane);
+        if constexpr (WLDS) mm_k<8, 4>(d8, duu, Wl, LDH, lane);
+        else mm_k<8, 4>(d8, duu, WuT, 64, lane);
         // dum = dm * [m > 0]; dh_direct -> DH (global scratch, own rows)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
@@ -560,8 +605,13 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
         // d[agg, e] = dum . Wm -> [node][128]
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        {
+          float4 am[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) mm_chunk<8>(d8, f4(Ms + c16 * LDH + 16 * c + 4 * s4), WmT, 64, 16 * c, lane);
+          for (int c = 0; c < 4; ++c) am[c] = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
+          if constexpr (WLDS) mm_k<8, 4>(d8, am, Wl + 128 * LDH, LDH, lane);
+          else mm_k<8, 4>(d8, am, WmT, 64, lane);
+        }
         wave_lds_sync();
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
@@ -617,6 +667,10 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
   }
 
   // ---- edge embedding (mpnn.py:89-104): due, dEagg ----
+  if constexpr (WLDS) {  // Wf^T; the last layer's readers finished at the barrier above
+    stage_rows<64 * NW>(Wl, LDH, P + PK_WFT, 64, 64, 64);
+    __syncthreads();
+  }
 #pragma unroll
   for (int ti = 0; ti < MAXT; ++ti) {
     const int t = w + ti * NWAVE;
@@ -636,8 +690,8 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
       f32x4 d4[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d4[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) mm_chunk<4>(d4, due[c], P + PK_WFT, 64, 16 * c, lane);
+      if constexpr (WLDS) mm_k<4, 4>(d4, due, Wl, LDH, lane);
+      else mm_k<4, 4>(d4, due, P + PK_WFT, 64, lane);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = t * 16 + 4 * s4 + rr;
@@ -650,16 +704,13 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
   __syncthreads();
   // dz_j = sum_{i in N(j)} G_i * [w_ij wa + z_j > 0];  dwa += same * w_ij
   {
-    float wa[16], wx[16][8];
+    float wa[16], wxr[8];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int f = 16 * c + 4 * s4 + i;
-        wa[4 * c + i] = P[PK_WA + f];
+      for (int i = 0; i < 4; ++i) wa[4 * c + i] = P[PK_WA + 16 * c + 4 * s4 + i];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) wx[4 * c + i][k] = P[PK_WX + f * 8 + k];
-      }
+    for (int k = 0; k < 8; ++k) wxr[k] = P[PK_WX + lane * 8 + k];
     float dwa[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwa[i] = 0.f;
@@ -667,21 +718,30 @@ __global__ __launch_bounds__(TPB) void mpnn_backward_kernel(MpnnArgs a) {
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
+        // Z = Wx.x of the tile's 16 nodes (same expression as forward phase A) into the wave scratch
+        for (int i = 0; i < 16; ++i) {
+          const int rr = t * 16 + i;
+          float zz = 0.f;
+          if (rr < rows_valid) {
+            const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + rr) * 8);
+            const float4 x0 = xp[0], x1 = xp[1];
+            zz = wxr[0] * x0.x + wxr[1] * x0.y + wxr[2] * x0.z + wxr[3] * x0.w + wxr[4] * x1.x + wxr[5] * x1.y +
+                 wxr[6] * x1.z + wxr[7] * x1.w;
+          }
+          Ms[i * LDH + lane] = zz;
+        }
+        wave_lds_sync();
         const int r = t * 16 + c16;
         const NodeRef n = node_ref(a, blk, r, rows_valid);
-        float xv[8];
-        {
-          const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + (n.valid ? r : 0)) * 8);
-          const float4 x0 = xp[0], x1 = xp[1];
-          xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w; xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
-        }
         float z[16], dz[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          z[i] = wx[i][0] * xv[0] + wx[i][1] * xv[1] + wx[i][2] * xv[2] + wx[i][3] * xv[3] + wx[i][4] * xv[4] +
-                 wx[i][5] * xv[5] + wx[i][6] * xv[6] + wx[i][7] * xv[7];
-          dz[i] = 0.f;
+        for (int c = 0; c < 4; ++c) {
+          const float4 zv = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
+          z[4 * c] = zv.x; z[4 * c + 1] = zv.y; z[4 * c + 2] = zv.z; z[4 * c + 3] = zv.w;
         }
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dz[i] = 0.f;
         const int rbase = n.gl * N;
         for (int q = n.e0; q < n.e1; ++q) {
           const uint32_t ex = n.ed[q];
@@ -783,11 +843,37 @@ extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
   return ((size_t)SV_NODE_TENSORS * n_spins * batch * 64 + 2 * (size_t)batch * 64) * sizeof(float);
 }
 
-static size_t lds_bytes(int N, int gpb, bool backward) {
-  const int rows_pad = (gpb * N + 15) & ~15;
-  size_t f = (size_t)rows_pad * LDH + (size_t)NWAVE * 16 * LDH;
-  if (backward) f += (size_t)gpb * 64 + NWAVE * 64;
+struct KCfg {
+  int nw, maxt;
+  bool wlds;
+  size_t lds;
+};
+constexpr size_t LDS_MAX = 160 * 1024;
+
+static size_t lds_bytes(int rows_pad, int gpb, int nw, bool wlds, bool backward) {
+  size_t f = (size_t)rows_pad * LDH + (size_t)nw * 16 * LDH;
+  if (wlds) f += backward ? (size_t)2 * 128 * LDH : (size_t)2 * 64 * LDW;
+  if (backward) f += (size_t)gpb * 64 + (size_t)nw * 64;
   return f * sizeof(float);
+}
+
+// 8 waves with LDS-staged weights when the block fits, else 4 waves (weights from L2).
+static KCfg pick_cfg(int N, int gpb, bool backward) {
+  const int rows_pad = (gpb * N + 15) & ~15;
+  const int ntiles = rows_pad / 16;
+  KCfg c;
+  for (int nw : {8, 4}) {
+    c.nw = nw;
+    c.wlds = true;
+    c.lds = lds_bytes(rows_pad, gpb, nw, true, backward);
+    c.maxt = (ntiles + nw - 1) / nw;
+    if (c.lds <= LDS_MAX && c.maxt <= 4) return c;
+  }
+  c.nw = 4;
+  c.wlds = false;
+  c.lds = lds_bytes(rows_pad, gpb, 4, false, backward);
+  c.maxt = (ntiles + 3) / 4;
+  return c;
 }
 
 extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
@@ -815,19 +901,22 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     call_maxdeg_kernel<<<min(256, (batch + 255) / 256), 256, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
   const int blocks = (batch + a.gpb - 1) / a.gpb;
-  const size_t lds = lds_bytes(N, a.gpb, false);
-  const int ntiles = ((a.gpb * N + 15) & ~15) / 16;
-#define ECO_LAUNCH_FWD(MT, SV)                                                                                  \
+  const KCfg k = pick_cfg(N, a.gpb, false);
+#define ECO_LAUNCH_FWD(MT, SV, NW, WL)                                                                          \
   do {                                                                                                         \
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<MT, SV>,                                        \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                          \
-    mpnn_forward_kernel<MT, SV><<<blocks, TPB, lds, st>>>(a);                                                  \
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<MT, SV, NW, WL>,                                \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)k.lds);                        \
+    mpnn_forward_kernel<MT, SV, NW, WL><<<blocks, 64 * NW, k.lds, st>>>(a);                                   \
   } while (0)
-  if (ntiles <= 4 * NWAVE) {
-    if (saved) ECO_LAUNCH_FWD(4, true); else ECO_LAUNCH_FWD(4, false);
-  } else {
-    if (saved) ECO_LAUNCH_FWD(8, true); else ECO_LAUNCH_FWD(8, false);
-  }
+#define ECO_LAUNCH_FWD2(MT, NW, WL) \
+  do { if (saved) ECO_LAUNCH_FWD(MT, true, NW, WL); else ECO_LAUNCH_FWD(MT, false, NW, WL); } while (0)
+  if (k.wlds && k.nw == 8 && k.maxt <= 2) ECO_LAUNCH_FWD2(2, 8, true);
+  else if (k.wlds && k.nw == 8) ECO_LAUNCH_FWD2(4, 8, true);
+  else if (k.wlds && k.maxt <= 4) ECO_LAUNCH_FWD2(4, 4, true);
+  else if (k.maxt <= 4) ECO_LAUNCH_FWD2(4, 4, false);
+  else if (k.maxt <= 8) ECO_LAUNCH_FWD2(8, 4, false);
+  else return fail(ECO_ERR_ARG, "graph block too large");
+#undef ECO_LAUNCH_FWD2
 #undef ECO_LAUNCH_FWD
   return check_launch("mpnn_forward");
 }
@@ -851,16 +940,19 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.dq = dq;
   a.gr = (float*)gradws;
   const int blocks = (batch + a.gpb - 1) / a.gpb;
-  const size_t lds = lds_bytes(a.N, a.gpb, true);
-  const int ntiles = ((a.gpb * a.N + 15) & ~15) / 16;
-  if (ntiles <= 4 * NWAVE) {
-    (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    mpnn_backward_kernel<4><<<blocks, TPB, lds, st>>>(a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    mpnn_backward_kernel<8><<<blocks, TPB, lds, st>>>(a);
-  }
+  const KCfg k = pick_cfg(a.N, a.gpb, true);
+#define ECO_LAUNCH_BWD(MT, NW, WL)                                                                              \
+  do {                                                                                                         \
+    (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<MT, NW, WL>,                                   \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)k.lds);                        \
+    mpnn_backward_kernel<MT, NW, WL><<<blocks, 64 * NW, k.lds, st>>>(a);                                      \
+  } while (0)
+  if (k.wlds && k.nw == 8 && k.maxt <= 2) ECO_LAUNCH_BWD(2, 8, true);
+  else if (k.wlds && k.nw == 8) ECO_LAUNCH_BWD(4, 8, true);
+  else if (k.wlds && k.maxt <= 4) ECO_LAUNCH_BWD(4, 4, true);
+  else if (k.maxt <= 4) ECO_LAUNCH_BWD(4, 4, false);
+  else if (k.maxt <= 8) ECO_LAUNCH_BWD(8, 4, false);
+  else return fail(ECO_ERR_ARG, "graph block too large");
+#undef ECO_LAUNCH_BWD
   return check_launch("mpnn_backward");
 }

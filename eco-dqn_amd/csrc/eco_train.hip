@@ -23,59 +23,88 @@ struct WJob {
 };
 constexpr int MAX_JOBS = 10;
 constexpr int WG_PER_JOB = 64;
-constexpr int SLABS_PER_JOB = WG_PER_JOB * NWAVE;
+constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
+constexpr int WROWS = 32;                  // rows per LDS tile
+constexpr int LDY = 68, LDX = 132;         // padded LDS row strides
 
 struct WJobs {
   WJob j[MAX_JOBS];
   int n;
 };
 
-__global__ __launch_bounds__(TPB) void wgrad_kernel(WJobs jobs, float* slabs) {
+// One workgroup (4 waves) reduces a contiguous row range of one job: 32-row tiles of dY and
+// X are staged in LDS with 16-byte coalesced loads; each wave owns up to two 32x32 output
+// tiles (o-tile, i-tile) and runs v_mfma_f32_32x32x2_f32 over the rows (k = row pair).
+__global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
+  __shared__ __attribute__((aligned(16))) float sY[WROWS * LDY];
+  __shared__ __attribute__((aligned(16))) float sX[WROWS * LDX];
   const WJob& J = jobs.j[blockIdx.y];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int jj = lane & 31, h = lane >> 5;
   const int K = J.K1 + J.K2;
-  const int chunk = ((J.R + WG_PER_JOB - 1) / WG_PER_JOB + 7) & ~7;
+  const int K4 = (K + 3) & ~3;
+  const int ntile = 2 * ((K + 31) / 32);
+  const int chunk = ((J.R + WG_PER_JOB - 1) / WG_PER_JOB + WROWS - 1) / WROWS * WROWS;
   const int r0 = blockIdx.x * chunk;
   const int r1 = min(J.R, r0 + chunk);
-  f32x16 acc[2][4];
+  f32x16 acc[2];
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot)
+  for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int it = 0; it < 4; ++it)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc[ot][it][k] = 0.f;
-  for (int rp = r0 + 2 * w; rp < r1; rp += 2 * NWAVE) {
-    const int r = rp + h;
-    const bool valid = r < r1;
-    const float a0 = valid ? J.dY[(size_t)r * 64 + jj] : 0.f;
-    const float a1 = valid ? J.dY[(size_t)r * 64 + 32 + jj] : 0.f;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      if (32 * it < K) {
-        const int col = 32 * it + jj;
-        float b = 0.f;
-        if (valid && col < K) b = col < J.K1 ? J.X1[(size_t)r * J.ld1 + col] : J.X2[(size_t)r * J.ld2 + col - J.K1];
-        acc[0][it] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[0][it], 0, 0, 0);
-        acc[1][it] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[1][it], 0, 0, 0);
-      }
+    for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
+  for (int rb = r0; rb < r1; rb += WROWS) {
+    // stage dY [32][64] and X [32][K4]
+    for (int i = threadIdx.x; i < WROWS * 16; i += 256) {
+      const int r = i >> 4, c = (i & 15) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rb + r < r1) v = *reinterpret_cast<const float4*>(J.dY + (size_t)(rb + r) * 64 + c);
+      *reinterpret_cast<float4*>(sY + r * LDY + c) = v;
     }
-  }
-  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x * NWAVE + w) * SLAB;
+    const int per = K4 >> 2;
+    for (int i = threadIdx.x; i < WROWS * per; i += 256) {
+      const int r = i / per, c = (i - r * per) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rb + r < r1) {
+        const size_t rr = (size_t)(rb + r);
+        v = c < J.K1 ? *reinterpret_cast<const float4*>(J.X1 + rr * J.ld1 + c)
+                     : *reinterpret_cast<const float4*>(J.X2 + rr * J.ld2 + (c - J.K1));
+      }
+      *reinterpret_cast<float4*>(sX + r * LDX + c) = v;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int ot = 0; ot < 2; ++ot)
+    for (int q = 0; q < 2; ++q) {
+      const int t = w + 4 * q;
+      if (t < ntile) {
+        const int ot = t & 1, it = t >> 1;
+        const int col = 32 * it + jj;
+        const bool cv = col < K;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      if (32 * it < K) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
-          slab[o * 128 + 32 * it + jj] = acc[ot][it][k];
+        for (int kk = 0; kk < WROWS / 2; ++kk) {
+          const int r = 2 * kk + h;
+          const float av = sY[r * LDY + 32 * ot + jj];
+          const float bv = cv ? sX[r * LDX + col] : 0.f;
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[q], 0, 0, 0);
         }
       }
     }
+    __syncthreads();
+  }
+  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x) * SLAB;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int t = w + 4 * q;
+    if (t < ntile) {
+      const int ot = t & 1, it = t >> 1;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
+        slab[o * 128 + 32 * it + jj] = acc[q][k];
+      }
+    }
+  }
 }
 
 // fixed-order sum of the slabs of every job into the flat gradient
@@ -91,13 +120,21 @@ __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad)
   grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
 }
 
-// column sums in fixed order: out[c] = sum_r X[r][c]
+// column sums in a fixed order: out[c * out_stride] = sum_r X[r][c]; one workgroup per column,
+// 256 strided partial sums combined by a fixed tree (bitwise reproducible)
 __global__ void colsum_kernel(const float* X, int R, int ld, int C, float* out, int out_stride) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float red[256];
+  const int c = blockIdx.x;
   if (c >= C) return;
   float acc = 0.f;
-  for (int r = 0; r < R; ++r) acc += X[(size_t)r * ld + c];
-  out[(size_t)c * out_stride] = acc;
+  for (int r = threadIdx.x; r < R; r += 256) acc += X[(size_t)r * ld + c];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s2 = 128; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[(size_t)c * out_stride] = red[0];
 }
 
 // ---------------------------------------------------------------------- TD ----
@@ -266,12 +303,12 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, 8, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
-  wgrad_kernel<<<dim3(WG_PER_JOB, n), TPB, 0, st>>>(J, slabs);
+  wgrad_kernel<<<dim3(WG_PER_JOB, n), 256, 0, st>>>(J, slabs);
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
-  colsum_kernel<<<1, 64, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
-  colsum_kernel<<<1, 64, 0, st>>>(DWRB, batch, 64, 64, grad + fo.Wr + 64, 1);
-  colsum_kernel<<<1, 64, 0, st>>>(DBR, batch, 1, 1, grad + fo.Br, 1);
-  colsum_kernel<<<1, 64, 0, st>>>(DWA, nblk, 64, 63, grad + fo.We, 1 + n_obs_in);
+  colsum_kernel<<<64, 256, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
+  colsum_kernel<<<64, 256, 0, st>>>(DWRB, batch, 64, 64, grad + fo.Wr + 64, 1);
+  colsum_kernel<<<1, 256, 0, st>>>(DBR, batch, 1, 1, grad + fo.Br, 1);
+  colsum_kernel<<<63, 256, 0, st>>>(DWA, nblk, 64, 63, grad + fo.We, 1 + n_obs_in);
   return check_launch("mpnn_backward_wgrad");
 }
 
