@@ -5,7 +5,7 @@ caller code (env_args dicts, experiments/train_eco.py:40-50) works unchanged.
 Graph generators keep the reference's class names and `get() -> ndarray[N,N] f64`
 contract (src/envs/utils.py:105-436); they draw from numpy's global RNG (the
 reference mixes numpy and networkx streams, which cannot be reproduced anyway).
-Batched training uses `GraphPool` (eco_hip/graphs.py) instead of per-episode draws.
+Batched training draws episodes from a device `GraphStore` pool (eco_hip/graphs.py) instead.
 """
 import random
 from abc import ABC, abstractmethod
@@ -122,6 +122,23 @@ class GraphGenerator(ABC):
     @abstractmethod
     def get(self, with_padding=False):
         raise NotImplementedError
+
+
+class RandomGraphGenerator(GraphGenerator):
+    """Density ~ U(0,1), then each pair connected with that probability (src/envs/utils.py:128-163)."""
+
+    def __init__(self, n_spins=20, edge_type=EdgeType.DISCRETE, biased=False):
+        if biased:
+            raise NotImplementedError("biased graphs are not on the MaxCut hot path")
+        super().__init__(n_spins, edge_type, False)
+
+    def get(self, with_padding=False):
+        n = self.n_spins
+        density = np.random.uniform()
+        iu, ju = np.triu_indices(n, 1)
+        keep = np.random.rand(iu.size) < density
+        iu, ju = iu[keep], ju[keep]
+        return _symmetric(n, iu, ju, _edge_weights(self.edge_type, iu.size))
 
 
 class RandomErdosRenyiGraphGenerator(GraphGenerator):
