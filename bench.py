@@ -158,10 +158,8 @@ def main():
     dt = time.perf_counter() - t0
     agent.network.timer = None
     agent.target_network.timer = None
-    if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = t.item()
+    from eco_hip.parallel import max_over_ranks
+    dt = max_over_ranks(dt, device=dev)
 
     # per-kernel roofline from the live events: forward launches vs backward launches
     kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}

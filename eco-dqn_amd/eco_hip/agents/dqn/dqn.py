@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ... import _lib
+from ...parallel import allreduce_gradients, broadcast_parameters
 from .utils import ReplayBuffer, TestMetric, set_global_seed
 
 
@@ -84,6 +85,9 @@ class DQN:
             self.load(init_network_params)
         elif init_weight_std is not None:
             self.network.init_normal_(init_weight_std, generator=torch.Generator().manual_seed(self.seed))
+        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        self.world = torch.distributed.get_world_size() if self.dist else 1
+        broadcast_parameters(self.network.flat)  # every rank starts from rank 0's weights
         self.target_network.load_state_dict(self.network.state_dict())
         n = self.network.flat.numel()
         self.grad = torch.zeros(n, dtype=torch.float32, device=self.device)
@@ -114,8 +118,6 @@ class DQN:
         self.save_network_frequency = save_network_frequency
         self.network_save_path = network_save_path
 
-        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
-        self.world = torch.distributed.get_world_size() if self.dist else 1
         self._act_counter = 0
         self._alloc_train_buffers(self.M)
 
@@ -204,10 +206,7 @@ class DQN:
                                        ctypes.c_float(self.gamma), int(bool(self.clip_Q_targets)), _lib.ptr(self.dq),
                                        _lib.ptr(self.sqerr), _lib.ptr(self.loss_dev), _lib.stream_ptr()))
         net.backward_graphs(xs, self.graphs, gid, self.saved, self.dq, self.grad, workspace=self.bw_ws)
-        scale = 1.0
-        if self.dist and self.world > 1:
-            torch.distributed.all_reduce(self.grad)  # RCCL sum over xGMI: 233.7 KB per step
-            scale = 1.0 / self.world
+        scale = allreduce_gradients(self.grad)  # RCCL sum over xGMI (233.7 KB), mean folded into Adam
         self.adam_step += 1
         _lib.check(_lib.lib.eco_adam(_lib.ptr(net.flat), _lib.ptr(self.grad), _lib.ptr(self.exp_avg),
                                      _lib.ptr(self.exp_avg_sq), net.flat.numel(), self.lr, 0.9, 0.999,
