@@ -403,6 +403,50 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   write_obs<VPT>(a, e, lane, s, h, tsf, c);
 }
 
+// Greedy solver action (src/agents/solver.py:100-131): the vertex with the largest immediate
+// cut change g = s * (J s) (first index on ties); an episode whose best change is negative is
+// finished (the solver stops, :124-127) and is marked done so later steps leave it unchanged.
+// Irreversible envs consider only still-flippable vertices (s == -1, :117-121).
+template <int VPT>
+__global__ __launch_bounds__(256) void env_greedy_kernel(EnvArgs a, int32_t* actions) {
+  const int lane = threadIdx.x & 63;
+  const int e = uniform_i(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (e >= a.B) return;
+  const int N = a.cfg.n_spins;
+  EpScal* sc = scal_ptr(a) + e;
+  if (sc->done) {
+    if (lane == 0) actions[e] = 0;
+    return;
+  }
+  const int8_t* gsp = (const int8_t*)(a.state + a.L.off_spins) + (size_t)e * N;
+  const int32_t* gh = (const int32_t*)(a.state + a.L.off_field) + (size_t)e * N;
+  int best = INT_MIN, bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) {
+      const int s = gsp[v];
+      if (a.cfg.reversible_spins || s < 0) {
+        const int g = s * gh[v];
+        if (g > best || (g == best && v < bi)) { best = g; bi = v; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int ob = __shfl_xor(best, o, 64), oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) {
+    if (best < 0 || bi == 0x7fffffff) {  // no improving (or no allowed) flip: solver stops
+      sc->done = 1;
+      actions[e] = 0;
+    } else {
+      actions[e] = bi;
+    }
+  }
+}
+
 // read-out of episode scalars / spins
 __global__ void env_read_kernel(EnvArgs a, double* scalars, int8_t* spins, int8_t* best) {
   const int e = blockIdx.x;
@@ -556,6 +600,17 @@ extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, 
   const int blocks = (batch + 3) / 4;
   ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, 0, st>>>(a)));
   return check_launch("env_step");
+}
+
+extern "C" int eco_env_greedy_actions(const eco_env_config* cfg, void* state, int32_t batch, int32_t* actions,
+                                      eco_stream_t stream) {
+  EnvArgs a;
+  int rc = make_args(a, cfg, nullptr, state, batch);
+  if (rc) return rc;
+  if (!actions) return fail(ECO_ERR_ARG, "null actions");
+  const int blocks = (batch + 3) / 4;
+  ECO_DISPATCH_VPT(cfg->n_spins, (env_greedy_kernel<V><<<blocks, 256, 0, (hipStream_t)stream>>>(a, actions)));
+  return check_launch("env_greedy");
 }
 
 extern "C" int eco_env_read(const eco_env_config* cfg, const void* state, int32_t batch, double* scalars,

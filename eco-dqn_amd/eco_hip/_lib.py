@@ -61,6 +61,7 @@ _SIG = {
                                     _P, _P]),
     "eco_env_read": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P, _P, _P]),
     "eco_check_errors": (ctypes.c_int, [_P]),
+    "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P]),
     "eco_mpnn_param_count": (ctypes.c_size_t, [_I]),
     "eco_mpnn_packed_count": (ctypes.c_size_t, []),
     "eco_mpnn_pack": (ctypes.c_int, [_P, _I, _P, _P]),

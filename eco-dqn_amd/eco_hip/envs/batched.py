@@ -129,6 +129,15 @@ class VecSpinSystem:
         self.obs_x = out
         return self.obs_x, self.rewards, self.dones
 
+    def greedy_actions(self, actions_out=None):
+        """Greedy solver step (solver.py:100-131): argmax of the immediate cut change per episode;
+        episodes without a non-negative change are marked done."""
+        out = actions_out if actions_out is not None else torch.empty(self.n_envs, dtype=torch.int32,
+                                                                      device=self.graphs.device)
+        _lib.check(_lib.lib.eco_env_greedy_actions(ctypes.byref(self.cfg), _lib.ptr(self.state), self.n_envs,
+                                                   _lib.ptr(out), self._s()))
+        return out
+
     def check_errors(self):
         _lib.check(_lib.lib.eco_check_errors(self._s()))
 

@@ -124,6 +124,12 @@ int eco_env_step(const eco_env_config *cfg, const eco_graph_set *gs, void *state
                  const int32_t *actions, double *rewards, uint8_t *dones, float *obs_x, double *obs_f64,
                  eco_stream_t stream);
 
+/* Greedy solver (src/agents/solver.py:88-131) for every episode: actions[B] = argmax of the
+ * immediate cut change (allowed vertices only when irreversible); episodes with no
+ * non-negative change are marked done (the solver stops). Step with eco_env_step. */
+int eco_env_greedy_actions(const eco_env_config *cfg, void *state, int32_t batch, int32_t *actions,
+                           eco_stream_t stream);
+
 /* Read-out of the env attributes callers use (dqn.py:564-566, experiments/utils.py:194-197):
  * scalars[B][8] = {current_step, score, normalized_score, best_score,
  *                  best_score_normalized, best_solution, hamming_to_best, done};

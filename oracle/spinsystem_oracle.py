@@ -233,3 +233,21 @@ class SpinSystemOracle:
     def state_rows(self):
         """The observation without the appended adjacency rows (obs[:n_obs])."""
         return self.get_observation()[:len(self.observables)]
+
+
+def greedy_solve(env):
+    """Greedy solver rule (src/agents/solver.py:100-131) on an oracle env after reset:
+    flip the vertex with the largest immediate cut change until that change is negative
+    (or the episode ends).  Returns the list of actions taken."""
+    acts = []
+    done = False
+    while not done:
+        mask = calculate_cut_changes(env.state[0, :], env.matrix)
+        if not env.reversible_spins:
+            mask = np.where(env.state[0, :] < 0, mask, np.finfo(np.float64).min)
+        a = int(mask.argmax())
+        if mask[a] < 0:
+            break
+        _, _, done, _ = env.step(a)
+        acts.append(a)
+    return acts

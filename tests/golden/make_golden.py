@@ -312,14 +312,46 @@ def make_greedy_rollout():
                         best_solution=np.float64(env.best_solution), best_score=np.float64(env.best_score))
 
 
+def make_greedy_solver():
+    """The reference Greedy solver rule (src/agents/solver.py:100-131) driven on the reference env:
+    action = argmax(env.scorer.get_score_mask(state)); stop when that change is negative.
+    (solver.py itself imports docplex, which is absent here, so its 10-line rule is applied
+    directly to the reference env/scorer objects.)"""
+    rng = np.random.default_rng(31)
+    out = {}
+    cases = []
+    for kind, n in (("ER", 20), ("ER", 20), ("ER", 200), ("BA", 60)):
+        J = graphs.er_graph(n, 0.15, rng) if kind == "ER" else graphs.ba_graph(n, 4, rng)
+        for init in ("minus", "random"):
+            spins = -np.ones(n, dtype=np.int64) if init == "minus" else 2 * rng.integers(0, 2, n) - 1
+            env = ising_env.make("SpinSystem", SingleGraphGenerator(J), 2 * n, **env_args("eco", n))
+            env.reset(spins=spins)
+            acts = []
+            done = False
+            while not done:
+                mask = env.scorer.get_score_mask(env.state[0, :env.n_spins], env.matrix)
+                a = int(mask.argmax())
+                if mask[a] < 0:
+                    break
+                _, _, done, _ = env.step(a)
+                acts.append(a)
+            cases.append((J, spins, acts, env.best_solution, env.best_score))
+    for i, (J, spins, acts, bsol, bsc) in enumerate(cases):
+        out[f"c{i}_J"] = J.astype(np.int8)
+        out[f"c{i}_spins"] = spins.astype(np.int8)
+        out[f"c{i}_actions"] = np.array(acts, dtype=np.int32)
+        out[f"c{i}_best_solution"] = np.float64(bsol)
+        out[f"c{i}_best_score"] = np.float64(bsc)
+    out["n_cases"] = np.int64(len(cases))
+    np.savez_compressed(os.path.join(HERE, "greedy_solver.npz"), **out)
+
+
 if __name__ == "__main__":
     random.seed(0)
     np.random.seed(0)
-    make_env_er20()
-    make_env_large()
-    make_mpnn()
-    make_dqn_step()
-    make_greedy_rollout()
+    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "greedy_rollout", "greedy_solver"]
+    for w in which:
+        globals()["make_" + w]()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -115,3 +115,16 @@ def test_dqn_train_step_matches_reference():
         assert abs(loss - float(f[p + "loss"])) <= 1e-6 * max(1.0, abs(float(f[p + "loss"])))
         for k in mo.KEYS:
             np.testing.assert_allclose(w[k].numpy(), f[p + "w/" + k], rtol=1e-5, atol=1e-7)
+
+
+def test_greedy_solver_matches_reference():
+    f = np.load(os.path.join(GOLDEN, "greedy_solver.npz"))
+    for c in range(int(f["n_cases"])):
+        p = f"c{c}_"
+        J = f[p + "J"].astype(np.float64)
+        n = J.shape[0]
+        env = so.SpinSystemOracle(J, 2 * n, basin_reward=1. / n)
+        env.reset(spins=f[p + "spins"].astype(np.int64))
+        acts = so.greedy_solve(env)
+        np.testing.assert_array_equal(acts, f[p + "actions"])
+        assert env.best_solution == f[p + "best_solution"]
