@@ -491,7 +491,7 @@ static int validate_gs(const eco_graph_set* gs, int N) {
   return ECO_OK;
 }
 
-static int32_t* err_word() {
+int32_t* err_word() {
   static int32_t* w = nullptr;  // one device word per process (read back after each call)
   if (!w) {
     if (hipMalloc(&w, sizeof(int32_t)) != hipSuccess) return nullptr;

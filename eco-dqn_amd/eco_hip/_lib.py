@@ -21,6 +21,7 @@ ECO_OK, ECO_ERR_ARG, ECO_ERR_HIP, ECO_ERR_PAST_END, ECO_ERR_BASIS, ECO_ERR_TARGE
 ECO_MAX_OBS = 8
 ECO_MAX_SPINS = 2048
 ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL = 0, 1
+ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
 
 
 class EnvConfig(ctypes.Structure):
@@ -54,6 +55,9 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int32
 _SIG = {
     "eco_graphs_prepare": (ctypes.c_int, [ctypes.POINTER(GraphSet), _P]),
+    "eco_graphs_generate_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
+    "eco_graphs_generate": (ctypes.c_int, [ctypes.POINTER(GraphSet), _I, _I, _I, ctypes.c_double, _I,
+                                           ctypes.c_uint64, ctypes.c_int64, _P, _P]),
     "eco_env_state_bytes": (ctypes.c_size_t, [ctypes.POINTER(EnvConfig), _I]),
     "eco_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvConfig), ctypes.POINTER(GraphSet), _P, _I, _P, _P, _P,
                                      ctypes.c_uint64, _P, _P, _P]),

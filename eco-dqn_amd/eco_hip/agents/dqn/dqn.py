@@ -39,7 +39,7 @@ class DQN:
                  final_exploration_step=1000000, adam_epsilon=1e-8, loss="mse", save_network_frequency=10000,
                  network_save_path='network', evaluate=True, test_envs=None, test_episodes=20,
                  test_frequency=10000, test_save_path='test_scores', test_metric=TestMetric.ENERGY_ERROR,
-                 logging=True, seed=None, train_minibatch=None, graph_pool_ids=None):
+                 logging=True, seed=None, train_minibatch=None, graph_pool_ids=None, regenerate_graphs=None):
         if isinstance(envs, (list, tuple)):
             if len(envs) != 1:
                 raise NotImplementedError("pass one VecSpinSystem (it already holds B episodes)")
@@ -107,6 +107,17 @@ class DQN:
         self._samples_since_sync = 0.0
         self.graph_pool_ids = (np.arange(self.graphs.n_graphs) if graph_pool_ids is None
                                else np.asarray(graph_pool_ids))
+        # Fresh graphs per episode like the reference's generators (utils.py:165-236): the store
+        # holds 2B slots, episode batch k runs on half k % 2 while the other half is regenerated on
+        # the device.  Replay entries reference graph ids, so the ring must not outlive one episode
+        # batch: capacity <= B * max_steps.
+        self.regenerate_graphs = regenerate_graphs
+        self._pool_half = 0
+        if regenerate_graphs is not None:
+            if self.graphs.n_graphs < 2 * envs.n_envs or not hasattr(self.graphs, "cap"):
+                raise ValueError("regenerate_graphs needs GraphStore.slots(2 * n_envs, ...)")
+            if replay_buffer_size > envs.n_envs * envs.max_steps:
+                raise ValueError("replay_buffer_size must be <= n_envs * max_steps when regenerating graphs")
         self._rng = np.random.default_rng(self.seed)
 
         self.evaluate = evaluate
@@ -222,6 +233,14 @@ class DQN:
         self.target_network.flat.copy_(self.network.flat)
 
     def _new_graph_ids(self, n):
+        if self.regenerate_graphs is not None:
+            kind, param = self.regenerate_graphs[:2]
+            weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
+            half = self._pool_half
+            self._pool_half ^= 1
+            self.graphs.generate(half * self.B, self.B, kind, param,
+                                 seed=int(self._rng.integers(1 << 62)), weights=weights)
+            return half * self.B + np.arange(n)
         return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
 
     def vector_step(self, is_training_ready):

@@ -96,21 +96,35 @@ def _ba_edges(n, m, rng):
     return np.array(iu, dtype=np.int64), np.array(ju, dtype=np.int64)
 
 
+def edge_cap(kind, n, param, slack_sd=10.0):
+    """Edge-slot size per graph for on-device generation: exact for BA (2 m (N - m)),
+    mean + slack_sd standard deviations for ER."""
+    if kind == "BA":
+        return 2 * int(param) * (n - int(param))
+    pairs = n * (n - 1) / 2.0
+    mean, sd = 2.0 * pairs * param, 2.0 * np.sqrt(pairs * param * (1 - param))
+    return int(mean + slack_sd * sd + 64)
+
+
 class GraphStore:
     """G graphs of N vertices resident on the device (eco_graph_set)."""
 
     def __init__(self, row_ptr, edge_base, edges, device="cuda", stream=None):
-        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
-        self.n_graphs, n1 = row_ptr.shape
+        dev = torch.device(device)
+        self.device = dev
+        if isinstance(row_ptr, torch.Tensor):
+            self.row_ptr, self.edge_base, self.edges = row_ptr, edge_base, edges
+            self.n_graphs, n1 = row_ptr.shape
+        else:
+            row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+            self.n_graphs, n1 = row_ptr.shape
+            self.row_ptr = torch.from_numpy(row_ptr).to(dev)
+            self.edge_base = torch.from_numpy(np.ascontiguousarray(edge_base, dtype=np.int64)).to(dev)
+            e = np.ascontiguousarray(edges, dtype=np.uint32).view(np.int32)
+            self.edges = torch.from_numpy(e if e.size else np.zeros(1, np.int32)).to(dev)
         self.n_spins = n1 - 1
         if self.n_spins > _lib.ECO_MAX_SPINS:
             raise ValueError(f"N={self.n_spins} exceeds ECO_MAX_SPINS={_lib.ECO_MAX_SPINS}")
-        dev = torch.device(device)
-        self.device = dev
-        self.row_ptr = torch.from_numpy(row_ptr).to(dev)
-        self.edge_base = torch.from_numpy(np.ascontiguousarray(edge_base, dtype=np.int64)).to(dev)
-        e = np.ascontiguousarray(edges, dtype=np.uint32).view(np.int32)
-        self.edges = torch.from_numpy(e if e.size else np.zeros(1, np.int32)).to(dev)
         self.deg = torch.zeros(self.n_graphs, self.n_spins, dtype=torch.int32, device=dev)
         self.max_deg = torch.zeros(self.n_graphs, dtype=torch.int32, device=dev)
         self.meta = torch.zeros(self.n_graphs, 4, dtype=torch.float64, device=dev)
@@ -119,6 +133,35 @@ class GraphStore:
                                 self.edges.data_ptr(), self.deg.data_ptr(), self.max_deg.data_ptr(),
                                 self.meta.data_ptr(), self.valid.data_ptr())
         _lib.check(_lib.lib.eco_graphs_prepare(ctypes.byref(self.gs), _lib.stream_ptr(stream)))
+
+    @classmethod
+    def slots(cls, n_graphs, n, cap, device="cuda"):
+        """Empty store with fixed edge slots (edge_base[g] = g * cap) for eco_graphs_generate."""
+        dev = torch.device(device)
+        rp = torch.zeros(n_graphs, n + 1, dtype=torch.int32, device=dev)
+        eb = torch.arange(n_graphs, dtype=torch.int64, device=dev) * int(cap)
+        ed = torch.zeros(max(1, n_graphs * int(cap)), dtype=torch.int32, device=dev)
+        st = cls(rp, eb, ed, device=dev)
+        st.cap = int(cap)
+        return st
+
+    @classmethod
+    def generated(cls, kind, n_graphs, n, param, seed=0, weights="discrete", device="cuda"):
+        """Pool of n_graphs ER(n, p=param) / BA(n, m=param) graphs generated on the device."""
+        st = cls.slots(n_graphs, n, edge_cap(kind, n, param), device=device)
+        st.generate(0, n_graphs, kind, param, seed, weights)
+        return st
+
+    def generate(self, first, count, kind, param, seed, weights="discrete", stream=None):
+        """Regenerate graphs [first, first+count) in place on the device (eco_graphs_generate)."""
+        if not hasattr(self, "cap"):
+            raise ValueError("generate() needs a store created with GraphStore.slots()")
+        ws = torch.empty(_lib.lib.eco_graphs_generate_workspace_bytes(self.n_spins, count), dtype=torch.uint8,
+                         device=self.device)
+        k = {"ER": _lib.ECO_GRAPH_ER, "BA": _lib.ECO_GRAPH_BA}[kind]
+        _lib.check(_lib.lib.eco_graphs_generate(ctypes.byref(self.gs), first, count, k, float(param),
+                                                int(weights == "discrete"), ctypes.c_uint64(seed), self.cap,
+                                                _lib.ptr(ws), _lib.stream_ptr(stream)))
 
     @classmethod
     def from_dense(cls, matrices, device="cuda"):

@@ -99,6 +99,17 @@ typedef struct {
  * and the MPNN degree normalisation (mpnn.py:34-38), computed on the device. */
 int eco_graphs_prepare(eco_graph_set *gs, eco_stream_t stream);
 
+/* On-device graph generation into graphs [first, first+count) of a set whose edge slots are
+ * fixed (edge_base[g] = g * edge_cap): the training-reset graph draws of
+ * RandomErdosRenyiGraphGenerator (kind ER, param = p) and RandomBarabasiAlbertGraphGenerator
+ * (kind BA, param = m) (src/envs/utils.py:165-236); +-1 weights when discrete_weights, else 1.
+ * Runs eco_graphs_prepare afterwards.  An edge-slot overflow is reported by eco_check_errors. */
+enum { ECO_GRAPH_ER = 1, ECO_GRAPH_BA = 2 };
+size_t eco_graphs_generate_workspace_bytes(int32_t n_spins, int32_t count);
+int eco_graphs_generate(eco_graph_set *gs, int32_t first, int32_t count, int32_t kind, double param,
+                        int32_t discrete_weights, uint64_t seed, int64_t edge_cap, void *workspace,
+                        eco_stream_t stream);
+
 /* ---- batched SpinSystem (spinsystem.py) ---- */
 
 /* Bytes of the opaque per-batch env state buffer (spins, local fields, counters,
