@@ -174,13 +174,82 @@ __device__ __forceinline__ void stage_rows(float* dst, int ldd, const float* __r
   }
 }
 
+// Per-row CSR info, staged in LDS once per block (instead of a dependent chain of global loads per
+// tile and phase): edge start within the graph, row length and the 0->1 clamped norm
+// (mpnn.py:36-37), packed as int2 {e0, len | norm << 16}; each graph's edge base and norm.max()
+// (per-graph scope of mpnn.py:102) sit in small per-graph arrays next to it.
+struct RowInfo {
+  int e0, e1, norm;
+};
+
+__device__ __forceinline__ int2 pack_row_info(const MpnnArgs& a, int blk, int r, int rows_valid) {
+  if (r >= rows_valid) return make_int2(0, 1 << 16);
+  const int gl = r / a.N, v = r - gl * a.N;
+  const int gid = a.gids[blk * a.gpb + gl];
+  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (a.N + 1);
+  const int b = rp[v], e = rp[v + 1];
+  const int nrm = max(a.gs.deg[(size_t)gid * a.N + v], 1);
+  return make_int2(b, (e - b) | (nrm << 16));
+}
+
+__device__ __forceinline__ RowInfo row_info(const int2* RI, int r) {
+  const int2 p = RI[r];
+  return RowInfo{p.x, p.x + (p.y & 0xFFFF), p.y >> 16};
+}
+
+// Visit the packed edges [e0, e1): groups of 4 edge words, the next group's loads issued before
+// the current group is consumed (one exposed load latency per 4 edges instead of per edge).
+template <typename F>
+__device__ __forceinline__ void for_edges(const uint32_t* __restrict__ edges, int e0, int e1, F&& f) {
+  int q = e0;
+  uint32_t cur[4], nxt[4];
+  if (q + 4 <= e1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = edges[q + k];
+  }
+  while (q + 4 <= e1) {
+    const bool more = q + 8 <= e1;
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) nxt[k] = edges[q + 4 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f(cur[k]);
+    q += 4;
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    }
+  }
+  for (; q < e1; ++q) f(edges[q]);
+}
+
+// sum_j w_ij * S[j][16c + 4(l>>4) + 0..3] over the CSR row (S: LDS rows of the block, stride LDH)
+__device__ __forceinline__ void gather_ri(const RowInfo& ri, const uint32_t* __restrict__ edges, const float* S,
+                                          int rbase, int s4, float4 (&acc)[4]) {
+  for_edges(edges, ri.e0, ri.e1, [&](uint32_t ex) {
+    const float wv = (float)edge_w(ex);
+    const float* hr = S + (rbase + edge_col(ex)) * LDH + 4 * s4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 hv = f4(hr + 16 * c);
+      acc[c].x = fmaf(wv, hv.x, acc[c].x);
+      acc[c].y = fmaf(wv, hv.y, acc[c].y);
+      acc[c].z = fmaf(wv, hv.z, acc[c].z);
+      acc[c].w = fmaf(wv, hv.w, acc[c].w);
+    }
+  });
+}
+
+
 // MAXT: max 16-node tiles per wave; NW: waves per workgroup; WLDS: stage each layer's weights in
 // LDS (one copy per workgroup, read as conflict-free ds_read_b128 B operands) instead of
 // streaming them from L2 in every wave.
+// LDS: Hs [rows_pad][LDH] | Wl [2][64][LDW] (WLDS) | Ms [NW][16][LDH] (x rows in phases A-C) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
 template <int MAXT, bool SAVE, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int NWAVE = NW;
+  constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int blk = blockIdx.x;
@@ -189,51 +258,68 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   const int rows_valid = g_valid * N;
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
-  float* Hs = lds;                                  // [rows_pad][LDH]
-  float* Wl = lds + rows_pad * LDH;                 // [2][64][LDW] staged weights (WLDS)
-  float* Ms = Wl + (WLDS ? 2 * 64 * LDW : 0) + w * 16 * LDH;  // per-wave [16][LDH]
-  if constexpr (WLDS) stage_rows<64 * NW>(Wl, LDH, a.P + PK_WF, 64, 64, 64);  // Wf, read after phase A's barrier
-  const size_t R0 = (size_t)blk * a.gpb * N;        // first global row of the block
-  const size_t RT = (size_t)a.B * N;                // rows of the call
+  float* Hs = lds;
+  float* Wl = lds + rows_pad * LDH;
+  float* Mreg = Wl + (WLDS ? 2 * 64 * LDW : 0);
+  float* Ms = Mreg + w * 16 * LDH;  // per-wave [16][LDH]
+  float* Xs = Mreg;                 // [rows_pad][8] node features (phases A-C)
+  int2* RI = reinterpret_cast<int2*>(Mreg + NW * 16 * LDH);
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);  // [gpb] per-graph edge base
+  int* MD = reinterpret_cast<int*>(GB + a.gpb);               // [gpb] per-graph max degree
+  float* Es = WLDS ? Wl : Mreg;     // phase-E scratch
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
   const float* P = a.P;
   const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  const uint32_t* __restrict__ edges = a.gs.edges;
+
+  // ---- staging: x rows, row info, Wf ----
+  for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
+    const int r = i >> 1;
+    float4 v = zero4();
+    if (r < rows_valid) v = f4(a.x + (R0 + r) * 8 + 4 * (i & 1));
+    st4(Xs + 8 * r + 4 * (i & 1), v);
+  }
+  for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
+    const int gid = a.gids[blk * a.gpb + gl];
+    GB[gl] = a.gs.edge_base[gid];
+    MD[gl] = a.gs.max_deg[gid];
+  }
+  if constexpr (WLDS) stage_rows<NT>(Wl, LDH, P + PK_WF, 64, 64, 64);
+  __syncthreads();
 
   // ---- phase A: Z = Wx . x  (edge-embedding node term) into Hs ----
   {
     float wx[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) wx[k] = P[PK_WX + lane * 8 + k];
-    for (int r = w; r < rows_pad; r += NWAVE) {
-      float z = 0.f;
-      if (r < rows_valid) {
-        const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + r) * 8);
-        const float4 x0 = xp[0], x1 = xp[1];
-        z = wx[0] * x0.x + wx[1] * x0.y + wx[2] * x0.z + wx[3] * x0.w + wx[4] * x1.x + wx[5] * x1.y + wx[6] * x1.z +
-            wx[7] * x1.w;
-      }
-      Hs[r * LDH + lane] = z;
+    for (int r = w; r < rows_pad; r += NW) {
+      const float4 x0 = f4(Xs + 8 * r), x1 = f4(Xs + 8 * r + 4);
+      Hs[r * LDH + lane] = wx[0] * x0.x + wx[1] * x0.y + wx[2] * x0.z + wx[3] * x0.w + wx[4] * x1.x +
+                           wx[5] * x1.y + wx[6] * x1.z + wx[7] * x1.w;
     }
   }
   __syncthreads();
 
   // ---- phase B: edge embedding (mpnn.py:89-104) -> E ----
   {
-    int maxdeg_call = 0;
-    if (a.norm_scope == ECO_NORM_PER_CALL) maxdeg_call = *a.call_maxdeg;
+    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
     float wa[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) wa[c * 4 + i] = P[PK_WA + 16 * c + 4 * s4 + i];
-    for (int t = w; t < ntiles; t += NWAVE) {
-      const int r = t * 16 + (lane & 15);
-      const NodeRef n = node_ref(a, blk, r, rows_valid);
+    for (int t = w; t < ntiles; t += NW) {
+      const int r = t * 16 + c16;
+      const RowInfo ri = row_info(RI, r);
+      const bool valid = r < rows_valid;
+      const int rbase = (r / N) * N;
       float4 acc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[c] = zero4();
-      const int rbase = n.gl * N;
-      for (int q = n.e0; q < n.e1; ++q) {
-        const uint32_t ex = n.ed[q];
+      for_edges(edges + (valid ? GB[r / N] : 0), ri.e0, ri.e1, [&](uint32_t ex) {
         const float wv = (float)edge_w(ex);
         const float* zr = Hs + (rbase + edge_col(ex)) * LDH + 4 * s4;
 #pragma unroll
@@ -244,16 +330,16 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
           acc[c].z += relu(fmaf(wv, wa[4 * c + 2], z.z));
           acc[c].w += relu(fmaf(wv, wa[4 * c + 3], z.w));
         }
-      }
-      const float nf = (float)n.norm;
+      });
+      const float nf = (float)ri.norm;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         acc[c].x = acc[c].x / nf; acc[c].y = acc[c].y / nf; acc[c].z = acc[c].z / nf; acc[c].w = acc[c].w / nf;
       }
       // feature 63 = norm / norm.max()  (mpnn.py:102)
-      const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : a.gs.max_deg[n.gid];
+      const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? MD[r / N] : 1);
       if (s4 == 3) acc[3].w = nf / (float)md;
-      if (!n.valid) {
+      if (!valid) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = zero4();
       } else if (SAVE) {
@@ -271,7 +357,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
         const int row = t * 16 + 4 * s4 + rr;
         if (row < rows_valid) {
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) a.E[(R0 + row) * 64 + nt * 16 + (lane & 15)] = relu(d[nt][rr]);
+          for (int nt = 0; nt < 4; ++nt) a.E[(R0 + row) * 64 + nt * 16 + c16] = relu(d[nt][rr]);
         }
       }
     }
@@ -283,16 +369,12 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     float w0[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) w0[k] = P[PK_W0 + lane * 8 + k];
-    for (int r = w; r < rows_pad; r += NWAVE) {
-      float z = 0.f;
-      if (r < rows_valid) {
-        const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + r) * 8);
-        const float4 x0 = xp[0], x1 = xp[1];
-        z = w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x + w0[5] * x1.y + w0[6] * x1.z +
-            w0[7] * x1.w;
-        if (SAVE) a.sv[(size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + lane] = relu(z);
-      }
-      Hs[r * LDH + lane] = relu(z);
+    for (int r = w; r < rows_pad; r += NW) {
+      const float4 x0 = f4(Xs + 8 * r), x1 = f4(Xs + 8 * r + 4);
+      const float z = relu(w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x +
+                           w0[5] * x1.y + w0[6] * x1.z + w0[7] * x1.w);
+      if (SAVE && r < rows_valid) a.sv[(size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + lane] = z;
+      Hs[r * LDH + lane] = z;
     }
   }
   __syncthreads();
@@ -302,32 +384,34 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     const float* Wm = P + PK_LAYER + layer * 16384;
     const float* Wu = Wm + 8192;
     if constexpr (WLDS) {  // the previous readers of Wl finished at the last barrier
-      stage_rows<64 * NW>(Wl, LDW, Wm, 128, 64, 128);
-      stage_rows<64 * NW>(Wl + 64 * LDW, LDW, Wu, 128, 64, 128);
+      stage_rows<NT>(Wl, LDW, Wm, 128, 64, 128);
+      stage_rows<NT>(Wl + 64 * LDW, LDW, Wu, 128, 64, 128);
       __syncthreads();
     }
     f32x4 hn[MAXT][4];
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
+      const int t = w + ti * NW;
       if (t < ntiles) {
-        const int r = t * 16 + (lane & 15);
-        const NodeRef n = node_ref(a, blk, r, rows_valid);
+        const int r = t * 16 + c16;
+        const RowInfo ri = row_info(RI, r);
+        const bool valid = r < rows_valid;
         // operand block of the message Linear: [agg (4 chunks), e (4 chunks)]; e is issued first
         float4 am[8];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) am[4 + c] = n.valid ? f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
+        for (int c = 0; c < 4; ++c) am[4 + c] = valid ? f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
         // aggregation (A . h) / norm, in A-operand layout
         float4 agg[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) agg[c] = zero4();
-        gather_rows(n, Hs, N, s4, agg);
-        const float nf = (float)n.norm;
+        gather_ri(ri, edges + (valid ? GB[r / N] : 0), Hs, (r / N) * N, s4, agg);
+        const float nf = (float)ri.norm;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           agg[c].x = agg[c].x / nf; agg[c].y = agg[c].y / nf; agg[c].z = agg[c].z / nf; agg[c].w = agg[c].w / nf;
+          am[c] = agg[c];
         }
-        if (SAVE && n.valid) {
+        if (SAVE && valid) {
           float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
           for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
@@ -336,8 +420,6 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
         f32x4 d[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) am[c] = agg[c];
         if constexpr (WLDS) mm_k<4, 8>(d, am, Wl, LDW, lane);
         else mm_k<4, 8>(d, am, Wm, 128, lane);
 #pragma unroll
@@ -346,9 +428,9 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
             const float mv = relu(d[nt][rr]);
-            Ms[(4 * s4 + rr) * LDH + nt * 16 + (lane & 15)] = mv;
+            Ms[(4 * s4 + rr) * LDH + nt * 16 + c16] = mv;
             if (SAVE && row < rows_valid)
-              a.sv[(size_t)(SV_M0 + layer) * RT * 64 + (R0 + row) * 64 + nt * 16 + (lane & 15)] = mv;
+              a.sv[(size_t)(SV_M0 + layer) * RT * 64 + (R0 + row) * 64 + nt * 16 + c16] = mv;
           }
         }
         wave_lds_sync();
@@ -359,7 +441,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           au[c] = f4(Hs + r * LDH + 16 * c + 4 * s4);
-          au[4 + c] = f4(Ms + (lane & 15) * LDH + 16 * c + 4 * s4);
+          au[4 + c] = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
         }
         if constexpr (WLDS) mm_k<4, 8>(hn[ti], au, Wl + 64 * LDW, LDW, lane);
         else mm_k<4, 8>(hn[ti], au, Wu, 128, lane);
@@ -369,7 +451,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     __syncthreads();
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
+      const int t = w + ti * NW;
       if (t < ntiles) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
@@ -377,9 +459,9 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
             const float hv = relu(hn[ti][nt][rr]);
-            Hs[row * LDH + nt * 16 + (lane & 15)] = hv;
+            Hs[row * LDH + nt * 16 + c16] = hv;
             if (SAVE && row < rows_valid)
-              a.sv[(size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + row) * 64 + nt * 16 + (lane & 15)] = hv;
+              a.sv[(size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + row) * 64 + nt * 16 + c16] = hv;
           }
         }
       }
@@ -387,82 +469,118 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     __syncthreads();
   }
 
-  // ---- phase E: ReadoutLayer (mpnn.py:143-159) + epsilon-greedy act ----
-  const float br = P[PK_BR];
-  for (int gl = w; gl < g_valid; gl += NWAVE) {
+  // ---- phase E: ReadoutLayer (mpnn.py:143-159) + epsilon-greedy act, spread over all waves ----
+  // column sums: all waves on each graph when there are fewer graphs than waves, else one wave per graph
+  const bool split = a.gpb < NW;
+  float* Red = Es;                                   // [gpb][NW][64] column-sum partials (split)
+  float* CG = Red + (split ? a.gpb * NW * 64 : 0);   // [gpb] relu(p) . wr[:64]
+  float* Qb = CG + ((a.gpb + 3) & ~3);               // [rows_pad] q values
+  if (split) {
+    for (int gl = 0; gl < g_valid; ++gl) {
+      const float* hg = Hs + gl * N * LDH;
+      float cs = 0.f;
+      for (int v = w; v < N; v += NW) cs += hg[v * LDH + lane];
+      Red[(gl * NW + w) * 64 + lane] = cs;
+    }
+    __syncthreads();
+  }
+  for (int gl = w; gl < g_valid; gl += NW) {
     const int e = blk * a.gpb + gl;
-    const float* hg = Hs + gl * N * LDH;
     float cs = 0.f;
-    for (int v = 0; v < N; ++v) cs += hg[v * LDH + lane];
+    if (split) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) cs += Red[(gl * NW + k) * 64 + lane];  // fixed order
+    } else {
+      const float* hg = Hs + gl * N * LDH;
+      for (int v = 0; v < N; ++v) cs += hg[v * LDH + lane];
+    }
     const float mean = cs / (float)N;
-    float p = 0.f;
     const float* wp = P + PK_WP + lane * 64;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) p = fmaf(wp[k], __shfl(mean, k, 64), p);
+    float4 wr4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wr4[k] = f4(wp + 4 * k);
+    float p = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      p = fmaf(wr4[k].x, __shfl(mean, 4 * k + 0, 64), p);
+      p = fmaf(wr4[k].y, __shfl(mean, 4 * k + 1, 64), p);
+      p = fmaf(wr4[k].z, __shfl(mean, 4 * k + 2, 64), p);
+      p = fmaf(wr4[k].w, __shfl(mean, 4 * k + 3, 64), p);
+    }
     if (SAVE) {
       a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)e * 64 + lane] = mean;
       a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)a.B * 64 + (size_t)e * 64 + lane] = p;
     }
     const float cg = wave_sum_f(relu(p) * P[PK_WR + lane]);
+    if (lane == 0) CG[gl] = cg;
+  }
+  __syncthreads();
+  const float br = P[PK_BR];
+  for (int r = threadIdx.x; r < rows_valid; r += NT) {
+    const float* hr = Hs + r * LDH;
+    float ql = 0.f;
+#pragma unroll 4
+    for (int f = 0; f < 64; f += 4) {
+      const float4 hv = f4(hr + f);
+      ql = fmaf(hv.x, P[PK_WR + 64 + f], ql);
+      ql = fmaf(hv.y, P[PK_WR + 65 + f], ql);
+      ql = fmaf(hv.z, P[PK_WR + 66 + f], ql);
+      ql = fmaf(hv.w, P[PK_WR + 67 + f], ql);
+    }
+    const float qv = CG[r / N] + ql + br;
+    Qb[r] = qv;
+    if (a.q) a.q[R0 + r] = qv;
+  }
+  if (!a.has_act) return;
+  __syncthreads();
+  for (int gl = w; gl < g_valid; gl += NW) {
+    const int e = blk * a.gpb + gl;
     float bestq = -INFINITY;
     int besti = 0x7fffffff;
     int n_allowed = 0;
     for (int v0 = 0; v0 < N; v0 += 64) {
       const int v = v0 + lane;
-      float qv = -INFINITY;
       bool allowed = false;
+      float qv = -INFINITY;
       if (v < N) {
-        const float* hr = hg + v * LDH;
-        float ql = 0.f;
-#pragma unroll 4
-        for (int f = 0; f < 64; f += 4) {
-          const float4 hv = f4(hr + f);
-          ql = fmaf(hv.x, P[PK_WR + 64 + f], ql);
-          ql = fmaf(hv.y, P[PK_WR + 65 + f], ql);
-          ql = fmaf(hv.z, P[PK_WR + 66 + f], ql);
-          ql = fmaf(hv.w, P[PK_WR + 67 + f], ql);
-        }
-        qv = cg + ql + br;
-        if (a.q) a.q[(size_t)e * N + v] = qv;
-        allowed = a.act.reversible || (a.x[((size_t)e * N + v) * 8] == a.act.allowed_value);
+        qv = Qb[gl * N + v];
+        allowed = a.act.reversible || (a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value);  // Xs was reused by Ms
       }
       n_allowed += __popcll(__ballot(allowed));
       if (allowed && (qv > bestq || (qv == bestq && v < besti))) { bestq = qv; besti = v; }
     }
-    if (a.has_act) {
-      // first index of the max (torch argmax)
+    // first index of the max (torch argmax)
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float oq = __shfl_xor(bestq, o, 64);
-        const int oi = __shfl_xor(besti, o, 64);
-        if (oq > bestq || (oq == bestq && oi < besti)) { bestq = oq; besti = oi; }
-      }
-      int action = besti;
-      const uint64_t r0 = rng3(a.act.seed, a.act.counter, (uint64_t)e);
-      if (u01(r0) < a.act.epsilon && n_allowed > 0) {  // random.uniform(0,1) >= eps -> greedy
-        const uint64_t r1 = rng3(a.act.seed ^ 0xA5A5A5A5ull, a.act.counter, (uint64_t)e);
-        int k = (int)(r1 % (uint64_t)n_allowed);
-        if (a.act.reversible) {
-          action = k;
-        } else {
-          action = -1;  // k-th allowed vertex
-          for (int v0 = 0; v0 < N && action < 0; v0 += 64) {
-            const int v = v0 + lane;
-            const bool al = v < N && a.x[((size_t)e * N + v) * 8] == a.act.allowed_value;
-            const uint64_t bal = __ballot(al);
-            const int c = __popcll(bal);
-            if (k < c) {
-              uint64_t b = bal;
-              for (int i = 0; i < k; ++i) b &= b - 1;
-              action = v0 + __ffsll((long long)b) - 1;
-            } else {
-              k -= c;
-            }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float oq = __shfl_xor(bestq, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (oq > bestq || (oq == bestq && oi < besti)) { bestq = oq; besti = oi; }
+    }
+    int action = besti;
+    const uint64_t r0 = rng3(a.act.seed, a.act.counter, (uint64_t)e);
+    if (u01(r0) < a.act.epsilon && n_allowed > 0) {  // random.uniform(0,1) >= eps -> greedy
+      const uint64_t r1 = rng3(a.act.seed ^ 0xA5A5A5A5ull, a.act.counter, (uint64_t)e);
+      int k = (int)(r1 % (uint64_t)n_allowed);
+      if (a.act.reversible) {
+        action = k;
+      } else {
+        action = -1;  // k-th allowed vertex
+        for (int v0 = 0; v0 < N && action < 0; v0 += 64) {
+          const int v = v0 + lane;
+          const bool al = v < N && a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value;
+          const uint64_t bal = __ballot(al);
+          const int c = __popcll(bal);
+          if (k < c) {
+            uint64_t b = bal;
+            for (int i = 0; i < k; ++i) b &= b - 1;
+            action = v0 + __ffsll((long long)b) - 1;
+          } else {
+            k -= c;
           }
         }
       }
-      if (lane == 0) a.actions[e] = action;
     }
+    if (lane == 0) a.actions[e] = action;
   }
 }
 
@@ -854,6 +972,7 @@ static size_t lds_bytes(int rows_pad, int gpb, int nw, bool wlds, bool backward)
   size_t f = (size_t)rows_pad * LDH + (size_t)nw * 16 * LDH;
   if (wlds) f += backward ? (size_t)2 * 128 * LDH : (size_t)2 * 64 * LDW;
   if (backward) f += (size_t)gpb * 64 + (size_t)nw * 64;
+  else f += (size_t)rows_pad * 2 + 3 * (size_t)gpb;  // packed row info + per-graph edge base, max degree
   return f * sizeof(float);
 }
 
@@ -902,6 +1021,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   }
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(N, a.gpb, false);
+  if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");
 #define ECO_LAUNCH_FWD(MT, SV, NW, WL)                                                                          \
   do {                                                                                                         \
     (void)hipFuncSetAttribute((const void*)mpnn_forward_kernel<MT, SV, NW, WL>,                                \
@@ -941,6 +1061,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.gr = (float*)gradws;
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
+  if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");
 #define ECO_LAUNCH_BWD(MT, NW, WL)                                                                              \
   do {                                                                                                         \
     (void)hipFuncSetAttribute((const void*)mpnn_backward_kernel<MT, NW, WL>,                                   \
