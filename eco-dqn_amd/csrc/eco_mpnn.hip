@@ -116,53 +116,6 @@ __device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-struct NodeRef {
-  bool valid;
-  int gl, v, e, gid, e0, e1, norm;
-  const uint32_t* ed;
-};
-
-__device__ __forceinline__ NodeRef node_ref(const MpnnArgs& a, int blk, int r, int rows_valid) {
-  NodeRef n;
-  n.valid = r < rows_valid;
-  const int rr = n.valid ? r : 0;
-  n.gl = rr / a.N;
-  n.v = rr - n.gl * a.N;
-  n.e = blk * a.gpb + n.gl;
-  n.gid = a.gids[n.e];
-  const int32_t* rp = a.gs.row_ptr + (size_t)n.gid * (a.N + 1);
-  n.e0 = n.valid ? rp[n.v] : 0;
-  n.e1 = n.valid ? rp[n.v + 1] : 0;
-  n.norm = max(a.gs.deg[(size_t)n.gid * a.N + n.v], 1);  // mpnn.py:36-37
-  n.ed = a.gs.edges + a.gs.edge_base[n.gid];
-  return n;
-}
-
-__device__ __forceinline__ int node_norm(const MpnnArgs& a, int blk, int r, int rows_valid) {
-  if (r >= rows_valid) return 1;
-  const int gl = r / a.N;
-  const int gid = a.gids[blk * a.gpb + gl];
-  return max(a.gs.deg[(size_t)gid * a.N + (r - gl * a.N)], 1);
-}
-
-// Sum over the CSR row of node n of w * S[j][16c + 4(l>>4) + 0..3] (S: LDS, row stride LDH).
-__device__ __forceinline__ void gather_rows(const NodeRef& n, const float* S, int N, int s4, float4 (&acc)[4]) {
-  const int rbase = n.gl * N;
-  for (int q = n.e0; q < n.e1; ++q) {
-    const uint32_t ex = n.ed[q];
-    const float wv = (float)edge_w(ex);
-    const float* hr = S + (rbase + edge_col(ex)) * LDH + 4 * s4;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float4 hv = f4(hr + 16 * c);
-      acc[c].x = fmaf(wv, hv.x, acc[c].x);
-      acc[c].y = fmaf(wv, hv.y, acc[c].y);
-      acc[c].z = fmaf(wv, hv.z, acc[c].z);
-      acc[c].w = fmaf(wv, hv.w, acc[c].w);
-    }
-  }
-}
-
 // stage a rows x cols fp32 matrix (cols % 4 == 0) from global (row stride lds_) into LDS (row stride ldd)
 template <int NTHREADS>
 __device__ __forceinline__ void stage_rows(float* dst, int ldd, const float* __restrict__ src, int lds_, int rows,
@@ -589,10 +542,14 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 // forward saved in a.sv.  This kernel produces the activation gradients (the
 // pre-activation gradients dY of every Linear, stored [R][64]) and the small
 // per-graph / per-block partials; eco_train.hip reduces dW = sum_nodes dY^T X.
+// LDS: G [rows_pad][LDH] | Wl [128][LDH] (WLDS; one transposed weight at a time) |
+//      Mreg [NW][16][LDH] (dq rows at the start, Z tiles at the end) | Xs [rows_pad][8] (WLDS) |
+//      RI [rows_pad] int2 | GB [gpb] i64 | DMEAN [gpb][64] | RED [(gpb < NW ? gpb : 1)][NW][64]
 template <int MAXT, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NWAVE = NW;
+  constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int blk = blockIdx.x;
@@ -601,11 +558,17 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   const int rows_valid = g_valid * N;
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
-  float* G = lds;                                            // [rows_pad][LDH] gathered-gradient source
-  float* Wl = lds + rows_pad * LDH;                          // [2][128][LDH] staged W^T (WLDS)
-  float* Ms = Wl + (WLDS ? 2 * 128 * LDH : 0) + w * 16 * LDH;  // per-wave transpose scratch
-  float* DMEAN = Wl + (WLDS ? 2 * 128 * LDH : 0) + NWAVE * 16 * LDH;  // [gpb][64]
-  float* RED = DMEAN + a.gpb * 64;                           // [NWAVE][64] dwa partials
+  const bool split = a.gpb < NW;  // readout: all waves per graph
+  float* G = lds;                                   // gathered-gradient source / dum rows
+  float* Wl = G + rows_pad * LDH;                   // staged W^T (WLDS)
+  float* Mreg = Wl + (WLDS ? 128 * LDH : 0);
+  float* Ms = Mreg + w * 16 * LDH;                  // per-wave Z tile
+  float* DQ = Mreg;                                 // [rows_pad] dq of the block's rows (start only)
+  float* Xs = Mreg + NW * 16 * LDH;                 // [rows_pad][8] (WLDS)
+  int2* RI = reinterpret_cast<int2*>(Xs + (WLDS ? rows_pad * 8 : 0));
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  float* DMEAN = reinterpret_cast<float*>(GB + a.gpb);
+  float* RED = DMEAN + a.gpb * 64;
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
   const float* P = a.P;
@@ -613,6 +576,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   float* gr = a.gr;
   const int s4 = lane >> 4;
   const int c16 = lane & 15;
+  const uint32_t* __restrict__ edges = a.gs.edges;
   auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
   auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
   const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
@@ -623,12 +587,38 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   float* DBR = DWRB + (size_t)a.B * 64;
   float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
 
-  // ---- readout backward (mpnn.py:143-159) per graph ----
+  // ---- staging: dq rows, row info, edge bases, x rows ----
+  for (int r = threadIdx.x; r < rows_pad; r += NT) {
+    DQ[r] = r < rows_valid ? a.dq[R0 + r] : 0.f;
+    RI[r] = pack_row_info(a, blk, r, rows_valid);
+  }
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
+  if constexpr (WLDS) {
+    for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
+      const int r = i >> 1;
+      st4(Xs + 8 * r + 4 * (i & 1), r < rows_valid ? f4(a.x + (R0 + r) * 8 + 4 * (i & 1)) : zero4());
+    }
+  }
+  __syncthreads();
+
+  // ---- readout backward (mpnn.py:143-159) ----
+  // dWr[64:] = sum_v dq_v h3_v: spread over all waves when the block holds fewer graphs than waves
+  if (split) {
+    for (int gl = 0; gl < g_valid; ++gl) {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      float dwb = 0.f;
+      for (int v = w; v < N; v += NWAVE) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+      RED[(gl * NWAVE + w) * 64 + lane] = dwb;
+    }
+    __syncthreads();
+  }
   for (int gl = w; gl < g_valid; gl += NWAVE) {
     const int e = blk * a.gpb + gl;
-    const float* dqe = a.dq + (size_t)e * N;
     float s = 0.f;
-    for (int v = lane; v < N; v += 64) s += dqe[v];
+    for (int v = lane; v < N; v += 64) s += DQ[gl * N + v];
     const float S = wave_sum_f(s);                       // d(sum_i q_i) / d br ...
     const float p = PP[(size_t)e * 64 + lane];
     const float wr = P[PK_WR + lane];
@@ -637,14 +627,19 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     DWRA[(size_t)e * 64 + lane] = relu(p) * S;
     if (lane == 0) DBR[e] = S;
     float dmean = 0.f;
-#pragma unroll 8
+#pragma unroll 16
     for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
     DMEAN[gl * 64 + lane] = dmean / (float)N;
     float dwb = 0.f;
-    const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
-    for (int v = 0; v < N; ++v) {
-      const float dv = dqe[v];
-      if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+    if (split) {
+#pragma unroll
+      for (int k = 0; k < NWAVE; ++k) dwb += RED[(gl * NWAVE + k) * 64 + lane];  // fixed order
+    } else {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      for (int v = 0; v < N; ++v) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
     }
     DWRB[(size_t)e * 64 + lane] = dwb;
   }
@@ -660,7 +655,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     for (int c = 0; c < 4; ++c) dh[ti][c] = zero4();
     if (t < ntiles && r < rows_valid) {
       const int gl = r / N;
-      const float dqi = a.dq[R0 + r];
+      const float dqi = DQ[r];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int f = 16 * c + 4 * s4;
@@ -670,23 +665,23 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
       }
     }
   }
+  // DQ (aliasing Mreg) is dead from here on; the next barrier orders it before the Z tiles
 
   // ---- update layers in reverse (mpnn.py:114-120) ----
   for (int layer = 2; layer >= 0; --layer) {
     const float* WmT = P + PK_LAYERT + layer * 16384;  // [128][64]
     const float* WuT = WmT + 8192;                      // [128][64]
     if constexpr (WLDS) {  // previous readers of Wl finished at the last barrier
-      stage_rows<64 * NW>(Wl, LDH, WuT, 64, 128, 64);
-      stage_rows<64 * NW>(Wl + 128 * LDH, LDH, WmT, 64, 128, 64);
+      stage_rows<NT>(Wl, LDH, WuT, 64, 128, 64);
       __syncthreads();
     }
+    // (1) duu = dh' [h' > 0];  [dh_direct, dm] = duu . Wu;  dum = dm [m > 0] -> G rows
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
-        // duu = dh' * [h' > 0]
         float4 duu[4];
         const float* hnext = SV(SV_H0 + layer + 1) + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
@@ -696,13 +691,11 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
                                hv.z > 0.f ? dh[ti][c].z : 0.f, hv.w > 0.f ? dh[ti][c].w : 0.f);
           if (valid) st4(GR(GR_DUU0 + layer) + (R0 + r) * 64 + 4 * s4 + 16 * c, duu[c]);
         }
-        // d[h, m] = duu . Wu  -> [node][128]
         f32x4 d8[8];
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (WLDS) mm_k<8, 4>(d8, duu, Wl, LDH, lane);
         else mm_k<8, 4>(d8, duu, WuT, 64, lane);
-        // dum = dm * [m > 0]; dh_direct -> DH (global scratch, own rows)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int row = t * 16 + 4 * s4 + rr;
@@ -712,30 +705,40 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
           for (int nt = 0; nt < 4; ++nt) {
             const float mv = rv ? SV(SV_M0 + layer)[base + nt * 16] : 0.f;
             const float dum = mv > 0.f ? d8[4 + nt][rr] : 0.f;
-            Ms[(4 * s4 + rr) * LDH + nt * 16 + c16] = dum;
+            G[row * LDH + nt * 16 + c16] = dum;
             if (rv) {
               GR(GR_DUM0 + layer)[base + nt * 16] = dum;
               GR(GR_DH)[base + nt * 16] = d8[nt][rr];
             }
           }
         }
-        wave_lds_sync();
-        // d[agg, e] = dum . Wm -> [node][128]
+      }
+    }
+    __syncthreads();
+    if constexpr (WLDS) {
+      stage_rows<NT>(Wl, LDH, WmT, 64, 128, 64);
+      __syncthreads();
+    }
+    // (2) [dagg, de] = dum . Wm;  G rows <- dagg / norm (own rows: read before written, same wave)
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NWAVE;
+      if (t < ntiles) {
+        const int r = t * 16 + c16;
+        f32x4 d8[8];
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        {
-          float4 am[4];
+        float4 am[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) am[c] = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
-          if constexpr (WLDS) mm_k<8, 4>(d8, am, Wl + 128 * LDH, LDH, lane);
-          else mm_k<8, 4>(d8, am, WmT, 64, lane);
-        }
+        for (int c = 0; c < 4; ++c) am[c] = f4(G + r * LDH + 16 * c + 4 * s4);
+        if constexpr (WLDS) mm_k<8, 4>(d8, am, Wl, LDH, lane);
+        else mm_k<8, 4>(d8, am, WmT, 64, lane);
         wave_lds_sync();
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int row = t * 16 + 4 * s4 + rr;
           const bool rv = row < rows_valid;
-          const float nf = (float)node_norm(a, blk, row, rows_valid);
+          const float nf = (float)row_info(RI, row).norm;
           const size_t base = (R0 + row) * 64 + c16;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
@@ -749,17 +752,18 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
       }
     }
     __syncthreads();
-    // dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
+    // (3) dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
         const int r = t * 16 + c16;
-        const NodeRef n = node_ref(a, blk, r, rows_valid);
+        const bool valid = r < rows_valid;
+        const RowInfo ri = row_info(RI, r);
         float4 acc[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = n.valid ? f4(GR(GR_DH) + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
-        gather_rows(n, G, N, s4, acc);
+        for (int c = 0; c < 4; ++c) acc[c] = valid ? f4(GR(GR_DH) + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
+        gather_ri(ri, edges + (valid ? GB[r / N] : 0), G, (r / N) * N, s4, acc);
 #pragma unroll
         for (int c = 0; c < 4; ++c) dh[ti][c] = acc[c];
       }
@@ -786,7 +790,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
 
   // ---- edge embedding (mpnn.py:89-104): due, dEagg ----
   if constexpr (WLDS) {  // Wf^T; the last layer's readers finished at the barrier above
-    stage_rows<64 * NW>(Wl, LDH, P + PK_WFT, 64, 64, 64);
+    stage_rows<NT>(Wl, LDH, P + PK_WFT, 64, 64, 64);
     __syncthreads();
   }
 #pragma unroll
@@ -813,7 +817,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = t * 16 + 4 * s4 + rr;
-        const float nf = (float)node_norm(a, blk, row, rows_valid);
+        const float nf = (float)row_info(RI, row).norm;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) G[row * LDH + nt * 16 + c16] = row < rows_valid ? d4[nt][rr] / nf : 0.f;
       }
@@ -841,8 +845,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
           const int rr = t * 16 + i;
           float zz = 0.f;
           if (rr < rows_valid) {
-            const float4* xp = reinterpret_cast<const float4*>(a.x + (R0 + rr) * 8);
-            const float4 x0 = xp[0], x1 = xp[1];
+            const float* xr = WLDS ? Xs + 8 * rr : a.x + (R0 + rr) * 8;
+            const float4 x0 = f4(xr), x1 = f4(xr + 4);
             zz = wxr[0] * x0.x + wxr[1] * x0.y + wxr[2] * x0.z + wxr[3] * x0.w + wxr[4] * x1.x + wxr[5] * x1.y +
                  wxr[6] * x1.z + wxr[7] * x1.w;
           }
@@ -850,7 +854,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
         }
         wave_lds_sync();
         const int r = t * 16 + c16;
-        const NodeRef n = node_ref(a, blk, r, rows_valid);
+        const bool valid = r < rows_valid;
+        const RowInfo ri = row_info(RI, r);
         float z[16], dz[16];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -860,9 +865,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
         wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < 16; ++i) dz[i] = 0.f;
-        const int rbase = n.gl * N;
-        for (int q = n.e0; q < n.e1; ++q) {
-          const uint32_t ex = n.ed[q];
+        const int rbase = (r / N) * N;
+        for_edges(edges + (valid ? GB[r / N] : 0), ri.e0, ri.e1, [&](uint32_t ex) {
           const float wv = (float)edge_w(ex);
           const float* gi = G + (rbase + edge_col(ex)) * LDH + 4 * s4;
 #pragma unroll
@@ -877,8 +881,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
               dwa[k] = fmaf(gm, wv, dwa[k]);
             }
           }
-        }
-        if (n.valid) {
+        });
+        if (valid) {
           float* dzp = GR(GR_DZ) + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
           for (int c = 0; c < 4; ++c) st4(dzp + 16 * c, make_float4(dz[4 * c], dz[4 * c + 1], dz[4 * c + 2], dz[4 * c + 3]));
@@ -970,9 +974,14 @@ constexpr size_t LDS_MAX = 160 * 1024;
 
 static size_t lds_bytes(int rows_pad, int gpb, int nw, bool wlds, bool backward) {
   size_t f = (size_t)rows_pad * LDH + (size_t)nw * 16 * LDH;
-  if (wlds) f += backward ? (size_t)2 * 128 * LDH : (size_t)2 * 64 * LDW;
-  if (backward) f += (size_t)gpb * 64 + (size_t)nw * 64;
-  else f += (size_t)rows_pad * 2 + 3 * (size_t)gpb;  // packed row info + per-graph edge base, max degree
+  if (backward) {
+    if (wlds) f += (size_t)128 * LDH + (size_t)rows_pad * 8;  // one W^T + x rows
+    f += (size_t)rows_pad * 2 + 2 * (size_t)gpb;               // packed row info + per-graph edge base
+    f += (size_t)gpb * 64 + (size_t)(gpb < nw ? gpb : 1) * nw * 64;
+  } else {
+    if (wlds) f += (size_t)2 * 64 * LDW;
+    f += (size_t)rows_pad * 2 + 3 * (size_t)gpb;  // packed row info + per-graph edge base, max degree
+  }
   return f * sizeof(float);
 }
 
