@@ -20,6 +20,22 @@
 
 namespace eco {
 
+// Optional per-phase wall-clock stamps (make timing -> libecohip_timing.so; tools/phase_timing.py).
+// Slots [blk][0..15] forward, [blk][16..31] backward, first ECO_TS_BLOCKS blocks only.
+#ifdef ECO_PHASE_TIMING
+constexpr int ECO_TS_BLOCKS = 8192;
+__device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
+#define ECO_TS(k)                                                                                           \
+  do {                                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < ECO_TS_BLOCKS) eco_phase_ts[blockIdx.x * 32 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define ECO_TS(k) \
+  do {            \
+  } while (0)
+#endif
+
+
 __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= PK_TOTAL) return;
@@ -202,6 +218,7 @@ __device__ __forceinline__ void gather_ri(const RowInfo& ri, const uint32_t* __r
 template <int MAXT, bool SAVE, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(0);
   constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
@@ -242,6 +259,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   }
   if constexpr (WLDS) stage_rows<NT>(Wl, LDH, P + PK_WF, 64, 64, 64);
   __syncthreads();
+  ECO_TS(1);
 
   // ---- phase A: Z = Wx . x  (edge-embedding node term) into Hs ----
   {
@@ -255,6 +273,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     }
   }
   __syncthreads();
+  ECO_TS(2);
 
   // ---- phase B: edge embedding (mpnn.py:89-104) -> E ----
   {
@@ -316,6 +335,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     }
   }
   __syncthreads();
+  ECO_TS(3);
 
   // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55) into Hs ----
   {
@@ -331,6 +351,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     }
   }
   __syncthreads();
+  ECO_TS(4);
 
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
   for (int layer = 0; layer < 3; ++layer) {
@@ -420,6 +441,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       }
     }
     __syncthreads();
+    ECO_TS(5 + layer);
   }
 
   // ---- phase E: ReadoutLayer (mpnn.py:143-159) + epsilon-greedy act, spread over all waves ----
@@ -484,6 +506,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     Qb[r] = qv;
     if (a.q) a.q[R0 + r] = qv;
   }
+  ECO_TS(8);
   if (!a.has_act) return;
   __syncthreads();
   for (int gl = w; gl < g_valid; gl += NW) {
@@ -535,6 +558,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     }
     if (lane == 0) a.actions[e] = action;
   }
+  ECO_TS(9);
 }
 
 // ============================================================== backward ====
@@ -548,6 +572,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 template <int MAXT, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(16);
   constexpr int NWAVE = NW;
   constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
@@ -600,6 +625,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     }
   }
   __syncthreads();
+  ECO_TS(17);
 
   // ---- readout backward (mpnn.py:143-159) ----
   // dWr[64:] = sum_v dq_v h3_v: spread over all waves when the block holds fewer graphs than waves
@@ -644,6 +670,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     DWRB[(size_t)e * 64 + lane] = dwb;
   }
   __syncthreads();
+  ECO_TS(18);
 
   // dh3 (A layout): dq_i * wr[64+f] + dmean_f / N
   float4 dh[MAXT][4];
@@ -769,6 +796,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
       }
     }
     __syncthreads();
+    ECO_TS(21 - layer);
   }
 
   // ---- h0 = relu(W0.x): du0 ----
@@ -824,6 +852,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     }
   }
   __syncthreads();
+  ECO_TS(22);
   // dz_j = sum_{i in N(j)} G_i * [w_ij wa + z_j > 0];  dwa += same * w_ij
   {
     float wa[16], wxr[8];
@@ -913,6 +942,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
       DWA[(size_t)blk * 64 + lane] = s;
     }
   }
+  ECO_TS(23);
 }
 
 __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, int B, int* out) {
@@ -940,6 +970,13 @@ static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco
 }  // namespace eco
 
 using namespace eco;
+
+#ifdef ECO_PHASE_TIMING
+extern "C" int eco_debug_phase_ts(unsigned long long* host, int32_t n) {
+  if (n > ECO_TS_BLOCKS * 32) n = ECO_TS_BLOCKS * 32;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(eco_phase_ts), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" size_t eco_mpnn_param_count(int32_t n_obs_in) {
   if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return 0;

@@ -1,0 +1,87 @@
+"""Per-phase timing of the MPNN forward/backward kernels (diagnostic, GPU only).
+
+Loads eco_hip/libecohip_timing.so (`make -C eco-dqn_amd timing`: the same kernels with
+wall_clock64() stamps at every block-wide barrier) and reports the mean duration of each
+phase over all blocks of one launch, for the bench's M=2048 ER-200 minibatch shape.
+
+usage: python tools/phase_timing.py [--batch 2048] [--n 200] [--p 0.15]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["ECO_HIP_LIB"] = os.environ.get("ECO_HIP_LIB") or os.path.join(ROOT, "eco-dqn_amd", "eco_hip", "libecohip_timing.so")
+sys.path.insert(0, os.path.join(ROOT, "eco-dqn_amd"))
+
+import torch  # noqa: E402
+
+from eco_hip import _lib  # noqa: E402
+from eco_hip.graphs import GraphStore  # noqa: E402
+from eco_hip.networks.mpnn import MPNN  # noqa: E402
+
+FWD = ["staging", "A: Z=Wx.x", "B: edge agg + Wf", "C: h0", "layer 0", "layer 1", "layer 2", "readout"]
+BWD = ["staging", "readout bwd", "layer 2", "layer 1", "layer 0", "du0 + due + Wf^T", "dz gather + dwa"]
+
+
+def stamps(nblk):
+    if not hasattr(_lib.lib, "eco_debug_phase_ts"):
+        return None
+    buf = (ctypes.c_ulonglong * (nblk * 32))()
+    _lib.lib.eco_debug_phase_ts.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    if _lib.lib.eco_debug_phase_ts(buf, nblk * 32):
+        raise RuntimeError("eco_debug_phase_ts failed")
+    return np.frombuffer(buf, dtype=np.uint64).reshape(nblk, 32).astype(np.int64)
+
+
+def report(title, ts, idx, names):
+    if ts is None:
+        print(f"{title}: (no stamps in this build)")
+        return
+    d = np.diff(ts[:, idx], axis=1) * 10.0 / 1000.0  # 100 MHz ticks -> us
+    span = (ts[:, idx[-1]].max() - ts[:, idx[0]].min()) * 10.0 / 1000.0
+    print(f"{title}: launch span {span:.1f} us, mean block {d.sum(1).mean():.1f} us")
+    for k, nm in enumerate(names):
+        print(f"  {nm:22s} {d[:, k].mean():8.2f} us  (p90 {np.percentile(d[:, k], 90):8.2f})")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--n", type=int, default=200)
+    ap.add_argument("--p", type=float, default=0.15)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, N = args.batch, args.n
+    store = GraphStore.generated("ER", B, N, args.p, seed=1, device=dev)
+    gids = torch.arange(B, dtype=torch.int32, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.zeros(B, N, 8)
+    x[:, :, 0] = torch.randint(0, 2, (B, N), generator=g).float() * 2 - 1
+    x[:, :, 1:7] = torch.rand(B, N, 6, generator=g)
+    x = x.to(dev)
+    net = MPNN(n_obs_in=7, device=dev)
+    net.init_normal_(0.01, generator=torch.Generator(device="cpu").manual_seed(0))
+    saved = torch.empty(MPNN.saved_bytes(N, B), dtype=torch.uint8, device=dev)
+    gpb = 1 if N >= 208 else 208 // N
+    nblk = (B + gpb - 1) // gpb
+    for _ in range(3):
+        net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL)
+    torch.cuda.synchronize()
+    report(f"forward (no save) B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
+    q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
+    torch.cuda.synchronize()
+    report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
+    dq = torch.zeros_like(q)
+    dq[torch.arange(B), torch.randint(0, N, (B,))] = 1e-3
+    grad = torch.zeros_like(net.flat)
+    net.backward_graphs(x, store, gids, saved, dq, grad)
+    torch.cuda.synchronize()
+    report(f"backward          B={B} N={N}", stamps(nblk), list(range(16, 24)), BWD)
+
+
+if __name__ == "__main__":
+    main()
