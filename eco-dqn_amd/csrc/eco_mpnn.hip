@@ -97,7 +97,11 @@ __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 // acc[nt] += sum_c A_c * W[nt*16 + (l&15)][16c + 4(l>>4) + 0..3] over NC chunks of 16 k, with the
 // weight fragments of chunk c+1 loaded while chunk c's MFMAs run (one-chunk-ahead software
 // pipeline: without it every weight load is followed by s_waitcnt vmcnt(0)).
-template <int NT, int NC>
+// SW = false: acc[nt] = D[node][out] in the 16x16 C layout (row 4(l>>4)+r, col l&15).
+// SW = true: the weight is the A operand and the node tile the B operand, D[out][node]: lane l holds
+// node l&15, features 16nt + 4(l>>4) + r -- exactly the operand layout of `a`, so a Linear's output
+// feeds the next Linear (or a row store) without a transpose.  Same products, same fma order.
+template <int NT, int NC, bool SW = false>
 __device__ __forceinline__ void mm_k(f32x4 (&acc)[NT], const float4 (&a)[NC], const float* __restrict__ W, int ldw,
                                      int lane) {
   const float* wp = W + (lane & 15) * ldw + 4 * (lane >> 4);
@@ -114,10 +118,17 @@ __device__ __forceinline__ void mm_k(f32x4 (&acc)[NT], const float4 (&a)[NC], co
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const float4 bb = b[c & 1][nt];
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].x, bb.x, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].y, bb.y, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].z, bb.z, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].w, bb.w, acc[nt], 0, 0, 0);
+      if constexpr (SW) {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.x, a[c].x, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.y, a[c].y, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.z, a[c].z, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.w, a[c].w, acc[nt], 0, 0, 0);
+      } else {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].x, bb.x, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].y, bb.y, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].z, bb.z, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].w, bb.w, acc[nt], 0, 0, 0);
+      }
     }
   }
 }
@@ -131,6 +142,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ float4 f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ float4 relu4(const f32x4& v) {
+  return make_float4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+}
+
+// forward LDS region after the weights: x rows (WLDS) or the readout scratch (weights from L2)
+__host__ __device__ constexpr int fwd_mreg_floats(int rows_pad, int gpb, int nw, bool wlds) {
+  return wlds ? rows_pad * 8 : (gpb < nw ? gpb * nw * 64 : 0) + ((gpb + 3) & ~3) + rows_pad;
+}
 
 // stage a rows x cols fp32 matrix (cols % 4 == 0) from global (row stride lds_) into LDS (row stride ldd)
 template <int NTHREADS>
@@ -214,7 +233,8 @@ __device__ __forceinline__ void gather_ri(const RowInfo& ri, const uint32_t* __r
 // MAXT: max 16-node tiles per wave; NW: waves per workgroup; WLDS: stage each layer's weights in
 // LDS (one copy per workgroup, read as conflict-free ds_read_b128 B operands) instead of
 // streaming them from L2 in every wave.
-// LDS: Hs [rows_pad][LDH] | Wl [2][64][LDW] (WLDS) | Ms [NW][16][LDH] (x rows in phases A-C) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
+// LDS: Hs [rows_pad][LDH] | Wl [2][64][LDW] (WLDS) | Xs [rows_pad][8] (WLDS) or readout scratch |
+//      RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
 template <int MAXT, bool SAVE, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -231,9 +251,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   float* Hs = lds;
   float* Wl = lds + rows_pad * LDH;
   float* Mreg = Wl + (WLDS ? 2 * 64 * LDW : 0);
-  float* Ms = Mreg + w * 16 * LDH;  // per-wave [16][LDH]
-  float* Xs = Mreg;                 // [rows_pad][8] node features (phases A-C)
-  int2* RI = reinterpret_cast<int2*>(Mreg + NW * 16 * LDH);
+  float* Xs = Mreg;                 // [rows_pad][8] node features (WLDS; else x is read from global)
+  int2* RI = reinterpret_cast<int2*>(Mreg + fwd_mreg_floats(rows_pad, a.gpb, NW, WLDS));
   int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);  // [gpb] per-graph edge base
   int* MD = reinterpret_cast<int*>(GB + a.gpb);               // [gpb] per-graph max degree
   float* Es = WLDS ? Wl : Mreg;     // phase-E scratch
@@ -244,13 +263,25 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   const int c16 = lane & 15;
   const uint32_t* __restrict__ edges = a.gs.edges;
 
-  // ---- staging: x rows, row info, Wf ----
-  for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
-    const int r = i >> 1;
-    float4 v = zero4();
-    if (r < rows_valid) v = f4(a.x + (R0 + r) * 8 + 4 * (i & 1));
-    st4(Xs + 8 * r + 4 * (i & 1), v);
+  // ---- staging: x rows (WLDS), row info, Wf ----
+  if constexpr (WLDS) {
+    for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
+      const int r = i >> 1;
+      float4 v = zero4();
+      if (r < rows_valid) v = f4(a.x + (R0 + r) * 8 + 4 * (i & 1));
+      st4(Xs + 8 * r + 4 * (i & 1), v);
+    }
   }
+  // node features of row r (zero for padding rows)
+  auto xrow = [&](int r, float4& x0, float4& x1) {
+    if constexpr (WLDS) {
+      x0 = f4(Xs + 8 * r);
+      x1 = f4(Xs + 8 * r + 4);
+    } else {
+      x0 = r < rows_valid ? f4(a.x + (R0 + r) * 8) : zero4();
+      x1 = r < rows_valid ? f4(a.x + (R0 + r) * 8 + 4) : zero4();
+    }
+  };
   for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
   for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
     const int gid = a.gids[blk * a.gpb + gl];
@@ -267,7 +298,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
     for (int k = 0; k < 8; ++k) wx[k] = P[PK_WX + lane * 8 + k];
     for (int r = w; r < rows_pad; r += NW) {
-      const float4 x0 = f4(Xs + 8 * r), x1 = f4(Xs + 8 * r + 4);
+      float4 x0, x1;
+      xrow(r, x0, x1);
       Hs[r * LDH + lane] = wx[0] * x0.x + wx[1] * x0.y + wx[2] * x0.z + wx[3] * x0.w + wx[4] * x1.x +
                            wx[5] * x1.y + wx[6] * x1.z + wx[7] * x1.w;
     }
@@ -322,15 +354,11 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (WLDS) mm_k<4, 4>(d, acc, Wl, LDH, lane);
-      else mm_k<4, 4>(d, acc, P + PK_WF, 64, lane);
+      if constexpr (WLDS) mm_k<4, 4, true>(d, acc, Wl, LDH, lane);
+      else mm_k<4, 4, true>(d, acc, P + PK_WF, 64, lane);
+      if (valid) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = t * 16 + 4 * s4 + rr;
-        if (row < rows_valid) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) a.E[(R0 + row) * 64 + nt * 16 + c16] = relu(d[nt][rr]);
-        }
+        for (int nt = 0; nt < 4; ++nt) st4(a.E + (R0 + r) * 64 + 16 * nt + 4 * s4, relu4(d[nt]));
       }
     }
   }
@@ -343,7 +371,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
     for (int k = 0; k < 8; ++k) w0[k] = P[PK_W0 + lane * 8 + k];
     for (int r = w; r < rows_pad; r += NW) {
-      const float4 x0 = f4(Xs + 8 * r), x1 = f4(Xs + 8 * r + 4);
+      float4 x0, x1;
+      xrow(r, x0, x1);
       const float z = relu(w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x +
                            w0[5] * x1.y + w0[6] * x1.z + w0[7] * x1.w);
       if (SAVE && r < rows_valid) a.sv[(size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + lane] = z;
@@ -390,36 +419,28 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 #pragma unroll
           for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
         }
-        // message = relu(Wm . [agg, e])
+        // message = relu(Wm . [agg, e]), produced in operand layout
         f32x4 d[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (WLDS) mm_k<4, 8>(d, am, Wl, LDW, lane);
-        else mm_k<4, 8>(d, am, Wm, 128, lane);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = t * 16 + 4 * s4 + rr;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const float mv = relu(d[nt][rr]);
-            Ms[(4 * s4 + rr) * LDH + nt * 16 + c16] = mv;
-            if (SAVE && row < rows_valid)
-              a.sv[(size_t)(SV_M0 + layer) * RT * 64 + (R0 + row) * 64 + nt * 16 + c16] = mv;
-          }
-        }
-        wave_lds_sync();
+        if constexpr (WLDS) mm_k<4, 8, true>(d, am, Wl, LDW, lane);
+        else mm_k<4, 8, true>(d, am, Wm, 128, lane);
         // h' = relu(Wu . [h, m])
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         float4 au[8];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           au[c] = f4(Hs + r * LDH + 16 * c + 4 * s4);
-          au[4 + c] = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
+          au[4 + c] = relu4(d[c]);
         }
-        if constexpr (WLDS) mm_k<4, 8>(hn[ti], au, Wl + 64 * LDW, LDW, lane);
-        else mm_k<4, 8>(hn[ti], au, Wu, 128, lane);
-        wave_lds_sync();
+        if (SAVE && valid) {
+          float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) st4(sm + 16 * c, au[4 + c]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (WLDS) mm_k<4, 8, true>(hn[ti], au, Wl + 64 * LDW, LDW, lane);
+        else mm_k<4, 8, true>(hn[ti], au, Wu, 128, lane);
       }
     }
     __syncthreads();
@@ -427,16 +448,12 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NW;
       if (t < ntiles) {
+        const int r = t * 16 + c16;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = t * 16 + 4 * s4 + rr;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const float hv = relu(hn[ti][nt][rr]);
-            Hs[row * LDH + nt * 16 + c16] = hv;
-            if (SAVE && row < rows_valid)
-              a.sv[(size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + row) * 64 + nt * 16 + c16] = hv;
-          }
+        for (int nt = 0; nt < 4; ++nt) {
+          const float4 hv = relu4(hn[ti][nt]);
+          st4(Hs + r * LDH + 16 * nt + 4 * s4, hv);
+          if (SAVE && r < rows_valid) st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, hv);
         }
       }
     }
@@ -520,7 +537,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       float qv = -INFINITY;
       if (v < N) {
         qv = Qb[gl * N + v];
-        allowed = a.act.reversible || (a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value);  // Xs was reused by Ms
+        allowed = a.act.reversible || (a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value);
       }
       n_allowed += __popcll(__ballot(allowed));
       if (allowed && (qv > bestq || (qv == bestq && v < besti))) { bestq = qv; besti = v; }
@@ -566,8 +583,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
 // forward saved in a.sv.  This kernel produces the activation gradients (the
 // pre-activation gradients dY of every Linear, stored [R][64]) and the small
 // per-graph / per-block partials; eco_train.hip reduces dW = sum_nodes dY^T X.
-// LDS: G [rows_pad][LDH] | Wl [128][LDH] (WLDS; one transposed weight at a time) |
-//      Mreg [NW][16][LDH] (dq rows at the start, Z tiles at the end) | Xs [rows_pad][8] (WLDS) |
+// LDS: G [rows_pad][LDH] (dq rows at the start) | Wl [2][128][LDH] (WLDS: Wu^T, Wm^T) | Xs [rows_pad][8] (WLDS) |
 //      RI [rows_pad] int2 | GB [gpb] i64 | DMEAN [gpb][64] | RED [(gpb < NW ? gpb : 1)][NW][64]
 template <int MAXT, int NW, bool WLDS>
 __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kernel(MpnnArgs a) {
@@ -584,12 +600,10 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
   const bool split = a.gpb < NW;  // readout: all waves per graph
-  float* G = lds;                                   // gathered-gradient source / dum rows
-  float* Wl = G + rows_pad * LDH;                   // staged W^T (WLDS)
-  float* Mreg = Wl + (WLDS ? 128 * LDH : 0);
-  float* Ms = Mreg + w * 16 * LDH;                  // per-wave Z tile
-  float* DQ = Mreg;                                 // [rows_pad] dq of the block's rows (start only)
-  float* Xs = Mreg + NW * 16 * LDH;                 // [rows_pad][8] (WLDS)
+  float* G = lds;                                   // gathered-gradient source rows
+  float* DQ = G;                                    // [rows_pad] dq of the block's rows (start only)
+  float* Wl = G + rows_pad * LDH;                   // staged Wu^T | Wm^T, [128][LDH] each (WLDS)
+  float* Xs = Wl + (WLDS ? 2 * 128 * LDH : 0);      // [rows_pad][8] (WLDS)
   int2* RI = reinterpret_cast<int2*>(Xs + (WLDS ? rows_pad * 8 : 0));
   int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
   float* DMEAN = reinterpret_cast<float*>(GB + a.gpb);
@@ -695,91 +709,73 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   // DQ (aliasing Mreg) is dead from here on; the next barrier orders it before the Z tiles
 
   // ---- update layers in reverse (mpnn.py:114-120) ----
+  // Every Linear runs with the weight as the MFMA A operand (mm_k<.., true>): outputs arrive in the
+  // node-operand layout (lane: node l&15, features 16c + 4(l>>4) + i), so the chain
+  // duu -> [dh_direct, dm] -> dum -> [dagg, de] needs no transpose and rows are stored as float4.
   for (int layer = 2; layer >= 0; --layer) {
     const float* WmT = P + PK_LAYERT + layer * 16384;  // [128][64]
     const float* WuT = WmT + 8192;                      // [128][64]
     if constexpr (WLDS) {  // previous readers of Wl finished at the last barrier
       stage_rows<NT>(Wl, LDH, WuT, 64, 128, 64);
+      stage_rows<NT>(Wl + 128 * LDH, LDH, WmT, 64, 128, 64);
       __syncthreads();
     }
-    // (1) duu = dh' [h' > 0];  [dh_direct, dm] = duu . Wu;  dum = dm [m > 0] -> G rows
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
-        float4 duu[4];
-        const float* hnext = SV(SV_H0 + layer + 1) + (R0 + r) * 64 + 4 * s4;
+        const size_t ro = (R0 + r) * 64 + 4 * s4;
+        // duu = dh' * [h' > 0]
+        float4 duu[4], mv[4];
+        const float* hnext = SV(SV_H0 + layer + 1) + ro;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const float4 hv = valid ? f4(hnext + 16 * c) : zero4();
+          mv[c] = valid ? f4(SV(SV_M0 + layer) + ro + 16 * c) : zero4();
           duu[c] = make_float4(hv.x > 0.f ? dh[ti][c].x : 0.f, hv.y > 0.f ? dh[ti][c].y : 0.f,
                                hv.z > 0.f ? dh[ti][c].z : 0.f, hv.w > 0.f ? dh[ti][c].w : 0.f);
-          if (valid) st4(GR(GR_DUU0 + layer) + (R0 + r) * 64 + 4 * s4 + 16 * c, duu[c]);
+          if (valid) st4(GR(GR_DUU0 + layer) + ro + 16 * c, duu[c]);
         }
+        // [dh_direct, dm] = duu . Wu
         f32x4 d8[8];
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (WLDS) mm_k<8, 4>(d8, duu, Wl, LDH, lane);
-        else mm_k<8, 4>(d8, duu, WuT, 64, lane);
+        if constexpr (WLDS) mm_k<8, 4, true>(d8, duu, Wl, LDH, lane);
+        else mm_k<8, 4, true>(d8, duu, WuT, 64, lane);
+        // dum = dm * [m > 0]
+        float4 dum[4];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = t * 16 + 4 * s4 + rr;
-          const bool rv = row < rows_valid;
-          const size_t base = (R0 + row) * 64 + c16;
+        for (int c = 0; c < 4; ++c) {
+          dum[c] = make_float4(mv[c].x > 0.f ? d8[4 + c][0] : 0.f, mv[c].y > 0.f ? d8[4 + c][1] : 0.f,
+                               mv[c].z > 0.f ? d8[4 + c][2] : 0.f, mv[c].w > 0.f ? d8[4 + c][3] : 0.f);
+          if (valid) {
+            st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
+            st4(GR(GR_DH) + ro + 16 * c, make_float4(d8[c][0], d8[c][1], d8[c][2], d8[c][3]));
+          }
+        }
+        // [dagg, de] = dum . Wm;  G rows <- dagg / norm  (d(agg)/d(A.h) = 1/norm)
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const float mv = rv ? SV(SV_M0 + layer)[base + nt * 16] : 0.f;
-            const float dum = mv > 0.f ? d8[4 + nt][rr] : 0.f;
-            G[row * LDH + nt * 16 + c16] = dum;
-            if (rv) {
-              GR(GR_DUM0 + layer)[base + nt * 16] = dum;
-              GR(GR_DH)[base + nt * 16] = d8[nt][rr];
-            }
+        for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (WLDS) mm_k<8, 4, true>(d8, dum, Wl + 128 * LDH, LDH, lane);
+        else mm_k<8, 4, true>(d8, dum, WmT, 64, lane);
+        const float nf = (float)row_info(RI, r).norm;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          st4(G + r * LDH + 16 * c + 4 * s4,
+              valid ? make_float4(d8[c][0] / nf, d8[c][1] / nf, d8[c][2] / nf, d8[c][3] / nf) : zero4());
+          if (valid) {
+            float* de = GR(GR_DE) + ro + 16 * c;
+            const float4 prev = layer == 2 ? zero4() : f4(de);
+            st4(de, make_float4(prev.x + d8[4 + c][0], prev.y + d8[4 + c][1], prev.z + d8[4 + c][2],
+                                prev.w + d8[4 + c][3]));
           }
         }
       }
     }
     __syncthreads();
-    if constexpr (WLDS) {
-      stage_rows<NT>(Wl, LDH, WmT, 64, 128, 64);
-      __syncthreads();
-    }
-    // (2) [dagg, de] = dum . Wm;  G rows <- dagg / norm (own rows: read before written, same wave)
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
-      if (t < ntiles) {
-        const int r = t * 16 + c16;
-        f32x4 d8[8];
-#pragma unroll
-        for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        float4 am[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) am[c] = f4(G + r * LDH + 16 * c + 4 * s4);
-        if constexpr (WLDS) mm_k<8, 4>(d8, am, Wl, LDH, lane);
-        else mm_k<8, 4>(d8, am, WmT, 64, lane);
-        wave_lds_sync();
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = t * 16 + 4 * s4 + rr;
-          const bool rv = row < rows_valid;
-          const float nf = (float)row_info(RI, row).norm;
-          const size_t base = (R0 + row) * 64 + c16;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            G[row * LDH + nt * 16 + c16] = rv ? d8[nt][rr] / nf : 0.f;  // d(agg)/d(A.h) = 1/norm
-            if (rv) {
-              float* de = GR(GR_DE) + base + nt * 16;
-              *de = (layer == 2 ? 0.f : *de) + d8[4 + nt][rr];
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // (3) dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
+    // dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
@@ -840,28 +836,24 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
       f32x4 d4[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d4[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (WLDS) mm_k<4, 4>(d4, due, Wl, LDH, lane);
-      else mm_k<4, 4>(d4, due, P + PK_WFT, 64, lane);
+      if constexpr (WLDS) mm_k<4, 4, true>(d4, due, Wl, LDH, lane);
+      else mm_k<4, 4, true>(d4, due, P + PK_WFT, 64, lane);
+      const float nf = (float)row_info(RI, r).norm;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = t * 16 + 4 * s4 + rr;
-        const float nf = (float)row_info(RI, row).norm;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) G[row * LDH + nt * 16 + c16] = row < rows_valid ? d4[nt][rr] / nf : 0.f;
-      }
+      for (int c = 0; c < 4; ++c)
+        st4(G + r * LDH + 16 * c + 4 * s4,
+            valid ? make_float4(d4[c][0] / nf, d4[c][1] / nf, d4[c][2] / nf, d4[c][3] / nf) : zero4());
     }
   }
   __syncthreads();
   ECO_TS(22);
   // dz_j = sum_{i in N(j)} G_i * [w_ij wa + z_j > 0];  dwa += same * w_ij
   {
-    float wa[16], wxr[8];
+    float wa[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) wa[4 * c + i] = P[PK_WA + 16 * c + 4 * s4 + i];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) wxr[k] = P[PK_WX + lane * 8 + k];
     float dwa[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwa[i] = 0.f;
@@ -869,29 +861,26 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     for (int ti = 0; ti < MAXT; ++ti) {
       const int t = w + ti * NWAVE;
       if (t < ntiles) {
-        // Z = Wx.x of the tile's 16 nodes (same expression as forward phase A) into the wave scratch
-        for (int i = 0; i < 16; ++i) {
-          const int rr = t * 16 + i;
-          float zz = 0.f;
-          if (rr < rows_valid) {
-            const float* xr = WLDS ? Xs + 8 * rr : a.x + (R0 + rr) * 8;
-            const float4 x0 = f4(xr), x1 = f4(xr + 4);
-            zz = wxr[0] * x0.x + wxr[1] * x0.y + wxr[2] * x0.z + wxr[3] * x0.w + wxr[4] * x1.x + wxr[5] * x1.y +
-                 wxr[6] * x1.z + wxr[7] * x1.w;
-          }
-          Ms[i * LDH + lane] = zz;
-        }
-        wave_lds_sync();
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
         const RowInfo ri = row_info(RI, r);
+        // z = Wx.x of the lane's node for its 16 features (same expression as forward phase A)
+        float4 x0 = zero4(), x1 = zero4();
+        if (valid) {
+          const float* xr = WLDS ? Xs + 8 * r : a.x + (R0 + r) * 8;
+          x0 = f4(xr);
+          x1 = f4(xr + 4);
+        }
         float z[16], dz[16];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 zv = f4(Ms + c16 * LDH + 16 * c + 4 * s4);
-          z[4 * c] = zv.x; z[4 * c + 1] = zv.y; z[4 * c + 2] = zv.z; z[4 * c + 3] = zv.w;
-        }
-        wave_lds_sync();
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float* wx = P + PK_WX + (16 * c + 4 * s4 + i) * 8;
+            const float4 w0 = f4(wx), w1 = f4(wx + 4);
+            z[4 * c + i] = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
+                           w1.z * x1.z + w1.w * x1.w;
+          }
 #pragma unroll
         for (int i = 0; i < 16; ++i) dz[i] = 0.f;
         const int rbase = (r / N) * N;
@@ -904,10 +893,10 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
             const float g4[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const int k = 4 * c + i;
-              const float gm = fmaf(wv, wa[k], z[k]) > 0.f ? g4[i] : 0.f;
-              dz[k] += gm;
-              dwa[k] = fmaf(gm, wv, dwa[k]);
+              const int kk = 4 * c + i;
+              const float gm = fmaf(wv, wa[kk], z[kk]) > 0.f ? g4[i] : 0.f;
+              dz[kk] += gm;
+              dwa[kk] = fmaf(gm, wv, dwa[kk]);
             }
           }
         });
@@ -1010,13 +999,14 @@ struct KCfg {
 constexpr size_t LDS_MAX = 160 * 1024;
 
 static size_t lds_bytes(int rows_pad, int gpb, int nw, bool wlds, bool backward) {
-  size_t f = (size_t)rows_pad * LDH + (size_t)nw * 16 * LDH;
+  size_t f = (size_t)rows_pad * LDH;
   if (backward) {
-    if (wlds) f += (size_t)128 * LDH + (size_t)rows_pad * 8;  // one W^T + x rows
+    if (wlds) f += (size_t)2 * 128 * LDH + (size_t)rows_pad * 8;  // Wu^T, Wm^T + x rows
     f += (size_t)rows_pad * 2 + 2 * (size_t)gpb;               // packed row info + per-graph edge base
     f += (size_t)gpb * 64 + (size_t)(gpb < nw ? gpb : 1) * nw * 64;
   } else {
     if (wlds) f += (size_t)2 * 64 * LDW;
+    f += (size_t)fwd_mreg_floats(rows_pad, gpb, nw, wlds);
     f += (size_t)rows_pad * 2 + 3 * (size_t)gpb;  // packed row info + per-graph edge base, max degree
   }
   return f * sizeof(float);
