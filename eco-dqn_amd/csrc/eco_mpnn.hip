@@ -18,6 +18,8 @@
 #include "eco_common.h"
 #include "eco_mpnn.h"
 
+#include <cstdlib>
+
 namespace eco {
 
 // Optional per-phase wall-clock stamps (make timing -> libecohip_timing.so; tools/phase_timing.py).
@@ -82,7 +84,6 @@ struct MpnnArgs {
   int norm_scope;
   const int* call_maxdeg;
   float* q;              // [B*N] or null
-  float* E;              // [B*N][64] (workspace, or the saved E tensor)
   float* sv;             // saved activations (training forward) or null
   int has_act;
   eco_act_config act;
@@ -115,21 +116,18 @@ __device__ __forceinline__ void mm_k(f32x4 (&acc)[NT], const float4 (&a)[NC], co
       for (int nt = 0; nt < NT; ++nt)
         b[(c + 1) & 1][nt] = *reinterpret_cast<const float4*>(wp + nt * 16 * ldw + 16 * (c + 1));
     }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float4 bb = b[c & 1][nt];
-      if constexpr (SW) {
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.x, a[c].x, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.y, a[c].y, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.z, a[c].z, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(bb.w, a[c].w, acc[nt], 0, 0, 0);
-      } else {
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].x, bb.x, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].y, bb.y, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].z, bb.z, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].w, bb.w, acc[nt], 0, 0, 0);
-      }
-    }
+    // kk outer, nt inner: consecutive MFMAs write different accumulators (no dependent-issue
+    // stall); each accumulator still sums its k in the same order.
+#define ECO_MM_STEP(K)                                                                           \
+  _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) {                                            \
+    if constexpr (SW) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[c & 1][nt].K, a[c].K, acc[nt], 0, 0, 0); \
+    else acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].K, b[c & 1][nt].K, acc[nt], 0, 0, 0);            \
+  }
+    ECO_MM_STEP(x)
+    ECO_MM_STEP(y)
+    ECO_MM_STEP(z)
+    ECO_MM_STEP(w)
+#undef ECO_MM_STEP
   }
 }
 
@@ -307,7 +305,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   __syncthreads();
   ECO_TS(2);
 
-  // ---- phase B: edge embedding (mpnn.py:89-104) -> E ----
+  // ---- phase B: edge embedding (mpnn.py:89-104) -> e (registers, operand layout) ----
+  float4 ereg[MAXT][4];
   {
     const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
     float wa[16];
@@ -315,7 +314,10 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) wa[c * 4 + i] = P[PK_WA + 16 * c + 4 * s4 + i];
-    for (int t = w; t < ntiles; t += NW) {
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NW;
+      if (t >= ntiles) break;
       const int r = t * 16 + c16;
       const RowInfo ri = row_info(RI, r);
       const bool valid = r < rows_valid;
@@ -356,9 +358,10 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (WLDS) mm_k<4, 4, true>(d, acc, Wl, LDH, lane);
       else mm_k<4, 4, true>(d, acc, P + PK_WF, 64, lane);
-      if (valid) {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) st4(a.E + (R0 + r) * 64 + 16 * nt + 4 * s4, relu4(d[nt]));
+      for (int nt = 0; nt < 4; ++nt) {
+        ereg[ti][nt] = relu4(d[nt]);  // the tile's e rows stay in this wave's registers for the layers
+        if (SAVE && valid) st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, ereg[ti][nt]);
       }
     }
   }
@@ -391,6 +394,14 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       stage_rows<NT>(Wl + 64 * LDW, LDW, Wu, 128, 64, 128);
       __syncthreads();
     }
+    if (layer == 0) ECO_TS(10);
+    // Half of each tile's MFMAs do not depend on the aggregation: Wm[:, 64:].e and Wu[:, :64].h.
+    // Waves with (w >> 2) even issue that half BEFORE their gather, the others after it, so each
+    // SIMD's MFMA pipe has work while its other waves gather from LDS (waves w, w+4 share a SIMD).
+    const bool mfma_first = ((w >> 2) & 1) == 0;
+    const float* WmL = WLDS ? Wl : Wm;
+    const float* WuL = WLDS ? Wl + 64 * LDW : Wu;
+    constexpr int ldw = WLDS ? LDW : 128;
     f32x4 hn[MAXT][4];
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
@@ -399,48 +410,57 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
         const int r = t * 16 + c16;
         const RowInfo ri = row_info(RI, r);
         const bool valid = r < rows_valid;
-        // operand block of the message Linear: [agg (4 chunks), e (4 chunks)]; e is issued first
-        float4 am[8];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) am[4 + c] = valid ? f4(a.E + (R0 + r) * 64 + 16 * c + 4 * s4) : zero4();
-        // aggregation (A . h) / norm, in A-operand layout
         float4 agg[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) agg[c] = zero4();
-        gather_ri(ri, edges + (valid ? GB[r / N] : 0), Hs, (r / N) * N, s4, agg);
+        const uint32_t* eg = edges + (valid ? GB[r / N] : 0);
+        if (!mfma_first) gather_ri(ri, eg, Hs, (r / N) * N, s4, agg);
+        // gather-independent half: d = Wm[:, 64:] . e ; hn = Wu[:, :64] . h
+        f32x4 d[4];
+        float4 hcur[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          hcur[nt] = f4(Hs + r * LDH + 16 * nt + 4 * s4);
+        }
+        mm_k<4, 4, true>(d, ereg[ti], WmL + 64, ldw, lane);
+        mm_k<4, 4, true>(hn[ti], hcur, WuL, ldw, lane);
+        if (layer == 0 && ti == 0) ECO_TS(11);
+        if (mfma_first) gather_ri(ri, eg, Hs, (r / N) * N, s4, agg);
+        if (layer == 0 && ti == 0) ECO_TS(12);
+        // aggregation (A . h) / norm (mpnn.py:118), already in operand layout
         const float nf = (float)ri.norm;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           agg[c].x = agg[c].x / nf; agg[c].y = agg[c].y / nf; agg[c].z = agg[c].z / nf; agg[c].w = agg[c].w / nf;
-          am[c] = agg[c];
         }
         if (SAVE && valid) {
           float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
           for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
         }
-        // message = relu(Wm . [agg, e]), produced in operand layout
-        f32x4 d[4];
+        // message = relu(Wm . [agg, e]) (mpnn.py:119)
+        mm_k<4, 4, true>(d, agg, WmL, ldw, lane);
+        float4 mrel[4];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (WLDS) mm_k<4, 8, true>(d, am, Wl, LDW, lane);
-        else mm_k<4, 8, true>(d, am, Wm, 128, lane);
-        // h' = relu(Wu . [h, m])
-        float4 au[8];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          au[c] = f4(Hs + r * LDH + 16 * c + 4 * s4);
-          au[4 + c] = relu4(d[c]);
-        }
+        for (int c = 0; c < 4; ++c) mrel[c] = relu4(d[c]);
         if (SAVE && valid) {
           float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) st4(sm + 16 * c, au[4 + c]);
+          for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
         }
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) hn[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (WLDS) mm_k<4, 8, true>(hn[ti], au, Wl + 64 * LDW, LDW, lane);
-        else mm_k<4, 8, true>(hn[ti], au, Wu, 128, lane);
+        // h' = relu(Wu . [h, m]) (mpnn.py:120)
+        mm_k<4, 4, true>(hn[ti], mrel, WuL + 64, ldw, lane);
+        if (layer == 0 && ti == 0) {
+          ECO_TS(13);
+#ifdef ECO_PHASE_TIMING
+#ifdef ECO_PHASE_TIMING
+          asm volatile("" ::"v"(hn[ti][3][3]));  // wait for the tile's last MFMA
+#endif
+#endif
+          ECO_TS(14);
+        }
       }
     }
     __syncthreads();
@@ -983,7 +1003,7 @@ extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packe
 
 extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
   if (n_spins < 1 || batch < 1) return 0;
-  return 256 + (size_t)n_spins * batch * 64 * sizeof(float);
+  return 256;  // the call-scope norm.max() slot
 }
 
 extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
@@ -1017,12 +1037,18 @@ static KCfg pick_cfg(int N, int gpb, bool backward) {
   const int rows_pad = (gpb * N + 15) & ~15;
   const int ntiles = rows_pad / 16;
   KCfg c;
-  for (int nw : {8, 4}) {
+  static const int force_nw = [] {
+    const char* e = getenv("ECO_MPNN_NW");
+    return e ? atoi(e) : 0;
+  }();
+  for (int nw : {16, 8, 4}) {
+    if (force_nw && nw != force_nw && nw != 4) continue;
+    if (backward && nw == 16) continue;  // the backward's 8-wide weight fragments need > 128 VGPRs
     c.nw = nw;
     c.wlds = true;
     c.lds = lds_bytes(rows_pad, gpb, nw, true, backward);
     c.maxt = (ntiles + nw - 1) / nw;
-    if (c.lds <= LDS_MAX && c.maxt <= 4) return c;
+    if (c.lds <= LDS_MAX && c.maxt <= (nw == 16 ? 1 : 4)) return c;
   }
   c.nw = 4;
   c.wlds = false;
@@ -1047,7 +1073,6 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   int* cmax = (int*)workspace;
   a.call_maxdeg = cmax;
   a.sv = (float*)saved;
-  a.E = saved ? a.sv + (size_t)SV_E * batch * N * 64 : (float*)((char*)workspace + 256);
   a.has_act = act != nullptr;
   if (act) a.act = *act;
   a.actions = actions;
@@ -1066,7 +1091,8 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   } while (0)
 #define ECO_LAUNCH_FWD2(MT, NW, WL) \
   do { if (saved) ECO_LAUNCH_FWD(MT, true, NW, WL); else ECO_LAUNCH_FWD(MT, false, NW, WL); } while (0)
-  if (k.wlds && k.nw == 8 && k.maxt <= 2) ECO_LAUNCH_FWD2(2, 8, true);
+  if (k.wlds && k.nw == 16 && k.maxt <= 1) ECO_LAUNCH_FWD2(1, 16, true);
+  else if (k.wlds && k.nw == 8 && k.maxt <= 2) ECO_LAUNCH_FWD2(2, 8, true);
   else if (k.wlds && k.nw == 8) ECO_LAUNCH_FWD2(4, 8, true);
   else if (k.wlds && k.maxt <= 4) ECO_LAUNCH_FWD2(4, 4, true);
   else if (k.maxt <= 4) ECO_LAUNCH_FWD2(4, 4, false);

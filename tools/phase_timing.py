@@ -71,7 +71,11 @@ def main():
     for _ in range(3):
         net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL)
     torch.cuda.synchronize()
-    report(f"forward (no save) B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
+    ts = stamps(nblk)
+    report(f"forward (no save) B={B} N={N}", ts, list(range(0, 9)), FWD)
+    if ts is not None and ts[:, 10].any():
+        report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
+               ["weight staging", "MFMA half 1 issue", "gather", "MFMA half 2", "(drain)", "to barrier"])
     q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
     torch.cuda.synchronize()
     report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
