@@ -23,7 +23,45 @@ constexpr int PK_WR = PK_WP + 4096;          // [128] layers_readout.0.weight
 constexpr int PK_BR = PK_WR + 128;           // [1]   layers_readout.0.bias
 constexpr int PK_WFT = PK_BR + 64;           // [64][64]  Wf^T          (backward)
 constexpr int PK_LAYERT = PK_WFT + 4096;     // + l*16384: Wm^T [128][64], +8192: Wu^T [128][64]
-constexpr int PK_TOTAL = PK_LAYERT + 3 * 16384;
+constexpr int PK_FP32_END = PK_LAYERT + 3 * 16384;
+// bf16 pieces (exact 3-way split W = W1 + W2 + W3) of the dense-path Linears as ready-made 16x16x32
+// A-operand fragments, a uint16 array starting at float PK_BF.  Per Linear: fragments
+// [half][piece p][nt][kc2] of 64 lanes x 8 bf16 (1 KB; lane l holds W_p[16nt + (l&15)][feature of
+// k' = 64 half + 32 kc2 + 8 (l>>4) + j], bf16_kprime_feature), so LDS-DMA copies them verbatim and every
+// operand read is one conflict-free ds_read_b128.  half = 64-input block (Wf: 1, Wm/Wu: 2).
+constexpr int PK_BF = (PK_FP32_END + 3) & ~3;
+constexpr int BF_FRAG = 512;                         // bf16 per fragment
+constexpr int BF_HALF = 3 * 4 * 2 * BF_FRAG;         // one 64-input half of a Linear (24 fragments)
+constexpr int BF_WF = 0;                             // edge_feature_NN: 1 half
+constexpr int BF_LAYER = BF_HALF;                    // + l * BF_LAYER_STRIDE: message (2 halves), then update
+constexpr int BF_LAYER_STRIDE = 4 * BF_HALF;
+constexpr int BF_TOTAL = BF_LAYER + 3 * BF_LAYER_STRIDE;  // bf16 elements
+constexpr int PK_TOTAL = PK_BF + BF_TOTAL / 2;
+
+// k' -> input feature of the bf16 Linear operands: within each 64-feature block, k' = 32kc + 8q + j
+// (kc = 0,1; q = lane >> 4; j = 0..7) holds feature 16(2kc + (j >> 2)) + 4q + (j & 3), i.e. the two
+// float4 registers c = 2kc, 2kc+1 of the f32 node-operand layout, so no lane exchange is needed.
+__host__ __device__ inline int bf16_kprime_feature(int kp) {
+  const int b = kp >> 6, r = kp & 63;
+  const int kc = r >> 5, q = (r >> 3) & 3, j = r & 7;
+  return 64 * b + 16 * (2 * kc + (j >> 2)) + 4 * q + (j & 3);
+}
+
+// Exact split v = p1 + p2 + p3 into bf16 bit patterns (truncation: each remainder is exact in f32,
+// the last one has <= 8 significant bits and is exact in bf16).
+__host__ __device__ inline void split3_bits(float v, uint16_t& p1, uint16_t& p2, uint16_t& p3) {
+  union { float f; uint32_t u; } a, b, c, d;
+  a.f = v;
+  b.u = a.u & 0xFFFF0000u;
+  c.f = v - b.f;
+  d.u = c.u & 0xFFFF0000u;
+  const float r2 = c.f - d.f;
+  union { float f; uint32_t u; } e;
+  e.f = r2;
+  p1 = (uint16_t)(b.u >> 16);
+  p2 = (uint16_t)(d.u >> 16);
+  p3 = (uint16_t)(e.u >> 16);
+}
 
 // ---- flat (state_dict order) parameter offsets, src/networks/mpnn.py ----
 struct FlatOffsets {

@@ -1,0 +1,485 @@
+// Dense-aggregation MPNN forward (src/networks/mpnn.py:40-159) for blocks of <= 224 rows with
+// +-1 edge weights (ER/BA EdgeType.DISCRETE / UNIFORM graphs, N <= 224: ER-20 ... ER-200).
+//
+// The CSR gather of eco_mpnn.hip reads one random 256-B embedding row per edge from LDS; 16 lanes
+// of a ds_read_b128 group hit 16 random rows, so at ER-200 density the gather is LDS-bank bound
+// and serialises with the Linears.  Here every aggregation is a dense MFMA product instead:
+//
+//   agg[f][i] = sum_j H[j][f] * A[j][i]      (A symmetric, entries 0/+-1, exact in bf16)
+//
+// with H split EXACTLY into three bf16 planes H = H1 + H2 + H3 (24 significand bits = fp32), so
+// every product is exact and the sums are fp32 MFMA accumulations: f32-exact products, f32 sums
+// (the reference's own fp32 bmm differs only in summation order).  The planes are stored
+// transposed, HT[p][f][j], so the A-operand fragment (8 consecutive j of one feature) is one
+// 16-B read; the B-operand fragment (8 adjacency entries of one node) is built in registers from
+// a per-row bitmask.  The 16x16 C layout of D[f][node] is exactly the node-operand layout of the
+// f32 Linears (lane: node l&15, features 16c + 4(l>>4) + r), so nothing is transposed.
+//
+// Edge layer (mpnn.py:89-104): with A in {0, +-1}, sum_j [A_ij != 0] relu(We.[A_ij, x_j]) =
+// A+ . relu(Z + w_a) + A- . relu(Z - w_a) (Z = Wx.x per node), two dense products over the same
+// plane buffer.  Linears stay on v_mfma_f32_16x16x4_f32 (exact f32) as in eco_mpnn.hip.
+//
+// One 1024-thread workgroup (16 waves) per block of whole graphs; wave w owns 16-node tile w and
+// keeps that tile's h and e in registers across the layers.
+// Included once by eco_mpnn.hip (same translation unit: shares the phase-timing buffer).
+#pragma once
+#include "eco_mpnn.h"
+#include "eco_mpnn_dev.h"
+
+namespace eco {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int DN_NW = 16;
+constexpr int DN_MAX_ROWS = 224;             // rows_pad limit (14 tiles, 7 k-chunks of 32)
+constexpr int DN_KC = 7;
+constexpr int DN_KPMAX = 224;                // plane rows (nodes j) per feature block
+constexpr int DN_PLANE = 4 * DN_KPMAX * 16;  // bf16 elements per plane: [4 feature blocks][j][16 features]
+constexpr int DN_ADJW = 2 * DN_KC;           // u32 words per adjacency row while it is built: {nz, neg} per chunk
+constexpr int DN_PL_BYTES = 3 * DN_PLANE * 2;
+constexpr int DN_WP_BYTES = 2 * BF_HALF * 2;  // a staged 128-input Linear (48 fragments)
+constexpr int DN_WX_BYTES = BF_HALF * 2;      // prefetched first half of the update Linear
+
+inline bool dense_eligible(const eco_graph_set* gs, int gpb) {
+  const int rows_pad = (gpb * gs->n_spins + 15) & ~15;
+  return gs->unit_weights && rows_pad <= DN_MAX_ROWS && gs->n_spins >= 4;
+}
+
+inline size_t dense_fwd_lds_bytes(int rows_pad, int gpb) {
+  return (size_t)DN_PL_BYTES + DN_WP_BYTES + DN_WX_BYTES + (size_t)rows_pad * 8 + (size_t)gpb * 12 + 16;
+}
+
+// Plane image: PL[p][ft][j][16] bf16 (feature block ft = f >> 4, 32-B rows); the 8-B piece of features
+// 4k .. 4k+3 of row j sits at piece position k ^ ((j >> 2) & 3), so 16 consecutive rows written by one
+// 16-lane group hit 16 distinct bank pairs, and the transposed reads of dense_agg stay conflict-free.
+__device__ __forceinline__ int plane_off(int ft, int j, int k) {
+  return ft * (DN_KPMAX * 16) + j * 16 + 4 * (k ^ ((j >> 2) & 3));
+}
+// store features 16ft + 4k .. +3 of node j as three exact bf16 pieces
+__device__ __forceinline__ void plane_store4(uint16_t* PL, int ft, int j, int k, float4 v) {
+  uint16_t a[4], b[4], c[4];
+  split3_bits(v.x, a[0], b[0], c[0]);
+  split3_bits(v.y, a[1], b[1], c[1]);
+  split3_bits(v.z, a[2], b[2], c[2]);
+  split3_bits(v.w, a[3], b[3], c[3]);
+  const int o = plane_off(ft, j, k);
+  *reinterpret_cast<uint2*>(PL + o) = make_uint2(a[0] | (uint32_t)a[1] << 16, a[2] | (uint32_t)a[3] << 16);
+  *reinterpret_cast<uint2*>(PL + DN_PLANE + o) = make_uint2(b[0] | (uint32_t)b[1] << 16, b[2] | (uint32_t)b[3] << 16);
+  *reinterpret_cast<uint2*>(PL + 2 * DN_PLANE + o) =
+      make_uint2(c[0] | (uint32_t)c[1] << 16, c[2] | (uint32_t)c[3] << 16);
+}
+
+// k-slot order of the aggregation MFMAs: lane group q, element jj <-> node 32kc + 16(jj >> 2) + 4q + (jj & 3)
+// (the rows the two transposed reads of dense_agg deliver).  Per lane and chunk the 8 adjacency entries
+// of those nodes for the lane's node are kept as 16 bits {nz byte, neg byte} (adj_bits16).
+__device__ __forceinline__ uint32_t adj_bits16(uint2 w, int q) {
+  const uint32_t nz = ((w.x >> (4 * q)) & 0xFu) | (((w.x >> (16 + 4 * q)) & 0xFu) << 4);
+  const uint32_t ng = ((w.y >> (4 * q)) & 0xFu) | (((w.y >> (16 + 4 * q)) & 0xFu) << 4);
+  return nz | (ng << 8);
+}
+// B fragment as bf16 0 / +1.0 / -1.0.  MODE 0: A (signed); 1: A+ = [A = +1]; 2: A- = [A = -1].
+template <int MODE>
+__device__ __forceinline__ bf16x8 adj_frag(uint32_t b16) {
+  const uint32_t nz = b16 & 0xFFu, ng = (b16 >> 8) & 0xFFu;
+  const uint32_t on = MODE == 0 ? nz : (MODE == 1 ? (nz & ~ng) : (nz & ng));
+  bf16x8 f;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    uint32_t v = ((on >> jj) & 1u) ? 0x3F80u : 0u;
+    if (MODE == 0) v |= ((ng >> jj) & 1u) << 15;
+    f[jj] = (short)v;
+  }
+  return f;
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// acc[ft] += sum over k-chunks [kc0, kc1) and the three planes of H[j][16ft + (l&15)] . A^(MODE)[j][node]:
+// acc[ft] = D[16ft + 4q + r][node l&15], the node-operand layout.  A fragments: two ds_read_b64_tr_b16
+// per (plane, ft) -- lane 4q'+p of each 16-lane group addresses row j = 32kc + 4q + q' (+16), piece p.
+// Call with EXEC all ones (wave-uniform conditions only).
+template <int MODE>
+__device__ __forceinline__ void dense_agg(f32x4 (&acc)[4], const uint16_t* PL, const uint32_t (&adjb)[4], int kc0,
+                                          int kc1, int lane) {
+  const int q = lane >> 4;
+  const int j_in = 4 * q + ((lane >> 2) & 3);
+  const int pc = (lane & 3) ^ q;  // piece position: (j >> 2) & 3 == q for every row read here
+#pragma unroll
+  for (int kc = 0; kc < DN_KC; ++kc) {
+    if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
+    const bf16x8 bf = adj_frag<MODE>((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+    const uint16_t* base = PL + (32 * kc + j_in) * 16 + 4 * pc;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        const uint16_t* a = base + p * DN_PLANE + ft * (DN_KPMAX * 16);
+        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
+        const bf16x8 af = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[ft], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float4 as_f4(const f32x4& v) { return make_float4(v[0], v[1], v[2], v[3]); }
+
+// 8 activations of the node-operand layout (float4 c = 2kc and 2kc+1 of a 64-feature block) as the
+// three exact bf16 pieces of a 16x16x32 B fragment (element j <-> feature of bf16_kprime_feature).
+__device__ __forceinline__ void split_frag(const float4& a, const float4& b, bf16x8& f1, bf16x8& f2, bf16x8& f3) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h1[8], h2[8], h3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h1[j] = __float_as_uint(v[j]) & 0xFFFF0000u;
+    const float r1 = v[j] - __uint_as_float(h1[j]);
+    h2[j] = __float_as_uint(r1) & 0xFFFF0000u;
+    h3[j] = __float_as_uint(r1 - __uint_as_float(h2[j]));
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 w1, w2, w3;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    w1[t] = (h1[2 * t] >> 16) | (h1[2 * t + 1] & 0xFFFF0000u);
+    w2[t] = (h2[2 * t] >> 16) | (h2[2 * t + 1] & 0xFFFF0000u);
+    w3[t] = (h3[2 * t] >> 16) | (h3[2 * t + 1] & 0xFFFF0000u);
+  }
+  f1 = __builtin_bit_cast(bf16x8, w1);
+  f2 = __builtin_bit_cast(bf16x8, w2);
+  f3 = __builtin_bit_cast(bf16x8, w3);
+}
+
+// acc[nt] += W[16nt + ..][one 64-input half] . x  on 16x16x32 bf16 MFMAs with both operands split in
+// three exact bf16 pieces; the six products above 2^-24 relative are kept (W3.X1, W2.X2, W1.X3, W2.X1,
+// W1.X2, W1.X1, smallest first), so each product carries f32 accuracy.  WH: the half's staged
+// fragments [p][nt][kc2] (BF_FRAG bf16 each, lane-linear) in LDS.
+__device__ __forceinline__ void mm_bf3(f32x4 (&acc)[4], const float4 (&x)[4], const uint16_t* WH, int lane) {
+  const uint16_t* wl = WH + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    bf16x8 x1, x2, x3;
+    split_frag(x[2 * kc2], x[2 * kc2 + 1], x1, x2, x3);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      const bf16x8 w3 = *reinterpret_cast<const bf16x8*>(wl + ((2 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3, x1, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x2, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x3, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x1, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x2, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, acc[nt], 0, 0, 0);
+    }
+  }
+}
+
+// LDS-DMA copy of n_frag 1-KB weight fragments (global -> LDS, both contiguous, no registers):
+// wave w issues fragments w, w + NW, ...  Retire with glds_wait() before the barrier that publishes them.
+template <int NW>
+__device__ __forceinline__ void glds_frags(uint16_t* dst, const uint16_t* src, int n_frag, int w, int lane) {
+  for (int f = w; f < n_frag; f += NW)
+    __builtin_amdgcn_global_load_lds((const void*)(src + f * BF_FRAG + lane * 8),
+                                     (__attribute__((address_space(3))) void*)(dst + f * BF_FRAG), 16, 0, 0);
+}
+__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
+//      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
+//      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
+template <bool SAVE>
+__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(0);
+  constexpr int NW = DN_NW;
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  const int KP = (rows_pad + 31) & ~31;  // plane rows touched by any k-chunk
+  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);  // [rows_pad][DN_ADJW] while the bitmask is built
+  uint16_t* WP = PL + 3 * DN_PLANE;
+  uint16_t* WX = WP + 2 * BF_HALF;
+  int2* RI = reinterpret_cast<int2*>(WX + BF_HALF);
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  int* MD = reinterpret_cast<int*>(GB + a.gpb);
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PB = reinterpret_cast<const uint16_t*>(P + PK_BF);
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  const uint32_t* __restrict__ edges = a.gs.edges;
+
+  // plane-mapped role (phases A-C): row j = 64 (w & 3) + lane, features 16 (w >> 2) .. +15
+  const int pj = 64 * (w & 3) + lane;
+  const int pft = w >> 2;
+  const bool pj_live = pj < KP;
+  const bool pj_valid = pj < rows_valid;
+  float4 xa = zero4(), xb = zero4();
+  if (pj_valid) {
+    xa = f4(a.x + (R0 + pj) * 8);
+    xb = f4(a.x + (R0 + pj) * 8 + 4);
+  }
+  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree, zeroed bitmask ----
+  glds_frags<NW>(WP, PB + BF_WF, 24, w, lane);
+  for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
+    const int gid = a.gids[blk * a.gpb + gl];
+    GB[gl] = a.gs.edge_base[gid];
+    MD[gl] = a.gs.max_deg[gid];
+  }
+  for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
+  __syncthreads();
+  ECO_TS(1);
+
+  // ---- adjacency bitmask (4 threads per row, 8 edge loads in flight per thread) ----
+  for (int i = threadIdx.x; i < rows_pad * 4; i += NT) {
+    const int r = i >> 2;
+    if (r >= rows_valid) continue;
+    const RowInfo ri = row_info(RI, r);
+    const int base = (r / N) * N;
+    const uint32_t* eg = edges + GB[r / N];
+    for (int e = ri.e0 + (i & 3); e < ri.e1; e += 32) {
+      uint32_t ex[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ex[k] = e + 4 * k < ri.e1 ? eg[e + 4 * k] : 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (e + 4 * k >= ri.e1) break;
+        const int j = base + edge_col(ex[k]);
+        const int wv = edge_w(ex[k]);
+        if (wv != 1 && wv != -1) atomicCAS(a.err, 0, ECO_ERR_GRAPH);  // the caller's unit_weights was wrong
+        uint32_t* word = ADJ + r * DN_ADJW + 2 * (j >> 5);
+        atomicOr(word, 1u << (j & 31));
+        if (wv < 0) atomicOr(word + 1, 1u << (j & 31));
+      }
+    }
+  }
+  __syncthreads();
+  // this lane's node and its k-chunk range; its adjacency bits move to registers
+  const bool has_tile = w < ntiles;
+  const int r = w * 16 + c16;
+  const bool valid = has_tile && r < rows_valid;
+  const int rr = min(r, rows_pad - 1);
+  const RowInfo ri = row_info(RI, rr);
+  const float nf = (float)ri.norm;
+  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  uint32_t adjb[4];
+  {
+    const uint2* arow = reinterpret_cast<const uint2*>(ADJ + rr * DN_ADJW);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = adj_bits16(arow[2 * k], s4);
+      const uint32_t hi = 2 * k + 1 < DN_KC ? adj_bits16(arow[2 * k + 1], s4) : 0u;
+      adjb[k] = lo | (hi << 16);
+    }
+  }
+  __syncthreads();  // bitmask region free for the planes
+
+  // ---- phase A: Z[j][f] = Wx[f] . x_j (weights uniform over the wave); U = relu(Z + w_a) planes ----
+  auto zval = [&](int f) {  // the CSR path's phase-A expression
+    const float* wx = P + PK_WX + f * 8;
+    return wx[0] * xa.x + wx[1] * xa.y + wx[2] * xa.z + wx[3] * xa.w + wx[4] * xb.x + wx[5] * xb.y + wx[6] * xb.z +
+           wx[7] * xb.w;
+  };
+  if (pj_live) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * pft + 4 * k + i;
+        u[i] = pj_valid ? relu(fmaf(1.f, P[PK_WA + f], zval(f))) : 0.f;
+      }
+      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    }
+  }
+  glds_wait();  // Wf fragments
+  __syncthreads();
+  ECO_TS(2);
+
+  // ---- phase B: edge embedding (mpnn.py:89-104): A+ . relu(Z + w_a) + A- . relu(Z - w_a) ----
+  f32x4 ea[4];
+#pragma unroll
+  for (int ft = 0; ft < 4; ++ft) ea[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (has_tile) dense_agg<1>(ea, PL, adjb, kc0, kc1, lane);
+  __syncthreads();
+  if (pj_live) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * pft + 4 * k + i;
+        u[i] = pj_valid ? relu(fmaf(-1.f, P[PK_WA + f], zval(f))) : 0.f;
+      }
+      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    }
+  }
+  __syncthreads();
+  float4 ereg[4];
+  {
+    if (has_tile) dense_agg<2>(ea, PL, adjb, kc0, kc1, lane);
+    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
+    float4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = make_float4(ea[c][0] / nf, ea[c][1] / nf, ea[c][2] / nf, ea[c][3] / nf);
+    // feature 63 = norm / norm.max()  (mpnn.py:102)
+    const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? MD[r / N] : 1);
+    if (s4 == 3) acc[3].w = nf / (float)md;
+    if (!valid) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = zero4();
+    } else if (SAVE) {
+      float* eap = a.sv + (size_t)SV_EAGG * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(eap + 16 * c, acc[c]);
+    }
+    f32x4 d[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) mm_bf3(d, acc, WP, lane);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      ereg[nt] = relu4(d[nt]);
+      if (SAVE && valid) st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, ereg[nt]);
+    }
+  }
+  __syncthreads();  // every wave is done with the V planes and with Wf
+  ECO_TS(3);
+
+  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55) as planes; the node-layout copy is read back ----
+  if (pj_live) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float* w0 = P + PK_W0 + (16 * pft + 4 * k + i) * 8;
+        const float h0 = w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
+                         w0[6] * xb.z + w0[7] * xb.w;
+        u[i] = pj_valid ? relu(h0) : 0.f;
+      }
+      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    }
+  }
+  __syncthreads();
+  float4 hreg[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {  // p1 + p2 + p3 reproduces the f32 value exactly
+    const int o = plane_off(c, rr, s4);
+    const uint2 u1 = *reinterpret_cast<const uint2*>(PL + o);
+    const uint2 u2 = *reinterpret_cast<const uint2*>(PL + DN_PLANE + o);
+    const uint2 u3 = *reinterpret_cast<const uint2*>(PL + 2 * DN_PLANE + o);
+    auto lo = [](uint32_t v) { return __uint_as_float(v << 16); };
+    auto hi = [](uint32_t v) { return __uint_as_float(v & 0xFFFF0000u); };
+    hreg[c] = make_float4(lo(u1.x) + lo(u2.x) + lo(u3.x), hi(u1.x) + hi(u2.x) + hi(u3.x),
+                          lo(u1.y) + lo(u2.y) + lo(u3.y), hi(u1.y) + hi(u2.y) + hi(u3.y));
+    if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
+  }
+  ECO_TS(4);
+
+  // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
+  // per layer: [planes h_l ready] DMA Wm -> WP and Wu(h-half) -> WX | aggregation MFMAs | [B1] message |
+  //            [B2] DMA Wu(m-half) -> WP | Wu(h-half).h | [B3] Wu(m-half).m, h' planes | [next layer]
+  for (int layer = 0; layer < 3; ++layer) {
+    const uint16_t* Wmb = PB + BF_LAYER + layer * BF_LAYER_STRIDE;
+    const uint16_t* Wub = Wmb + 2 * BF_HALF;
+    glds_frags<NW>(WP, Wmb, 48, w, lane);
+    glds_frags<NW>(WX, Wub, 24, w, lane);
+    f32x4 ag[4];
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) dense_agg<0>(ag, PL, adjb, kc0, kc1, lane);
+    float4 agg[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) agg[c] = make_float4(ag[c][0] / nf, ag[c][1] / nf, ag[c][2] / nf, ag[c][3] / nf);
+    if (SAVE && valid) {
+      float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
+    }
+    glds_wait();
+    __syncthreads();  // B1: Wm and Wu(h-half) landed
+    // message = relu(Wm . [agg, e])
+    f32x4 d[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) {
+      mm_bf3(d, ereg, WP + BF_HALF, lane);
+      mm_bf3(d, agg, WP, lane);
+    }
+    float4 mrel[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) mrel[c] = relu4(d[c]);
+    if (SAVE && valid) {
+      float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
+    }
+    __syncthreads();  // B2: all waves done with Wm and with the planes of h_layer
+    glds_frags<NW>(WP, Wub + BF_HALF, 24, w, lane);
+    // h' = relu(Wu . [h, m]): the h half while the m half lands
+    f32x4 hn[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) mm_bf3(hn, hreg, WX, lane);
+    glds_wait();
+    __syncthreads();  // B3
+    if (has_tile) mm_bf3(hn, mrel, WP, lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      hreg[c] = valid ? relu4(hn[c]) : zero4();
+      if (SAVE && valid) st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
+    }
+    if (layer < 2 && has_tile) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) plane_store4(PL, c, r, s4, hreg[c]);
+    }
+    __syncthreads();  // planes of h_{layer+1} complete; WP and WX free
+    ECO_TS(5 + layer);
+  }
+
+  // ---- phase E: readout + act over h3 rows staged as fp32 [rows][LDH] in the plane buffer ----
+  float* Hs = lds;
+  if (has_tile) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st4(Hs + r * LDH + 16 * c + 4 * s4, hreg[c]);
+  }
+  __syncthreads();
+  float* Scr = reinterpret_cast<float*>(WP);
+  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= DN_WP_BYTES;
+  readout_act<SAVE, NW>(a, Hs, LDH, Scr, split, blk, g_valid, rows_valid, R0, RT);
+  ECO_TS(8);
+}
+
+static int mpnn_forward_dense_launch(const MpnnArgs& a, bool save, hipStream_t st) {
+  const int rows_pad = (a.gpb * a.N + 15) & ~15;
+  const size_t lds = dense_fwd_lds_bytes(rows_pad, a.gpb);
+  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  if (save) {
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    mpnn_forward_dense_kernel<true><<<blocks, 64 * DN_NW, lds, st>>>(a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    mpnn_forward_dense_kernel<false><<<blocks, 64 * DN_NW, lds, st>>>(a);
+  }
+  return check_launch("mpnn_forward_dense");
+}
+
+}  // namespace eco

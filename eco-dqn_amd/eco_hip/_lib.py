@@ -37,7 +37,8 @@ class EnvConfig(ctypes.Structure):
 class GraphSet(ctypes.Structure):
     _fields_ = [("n_graphs", ctypes.c_int32), ("n_spins", ctypes.c_int32), ("row_ptr", ctypes.c_void_p),
                 ("edge_base", ctypes.c_void_p), ("edges", ctypes.c_void_p), ("deg", ctypes.c_void_p),
-                ("max_deg", ctypes.c_void_p), ("meta", ctypes.c_void_p), ("valid", ctypes.c_void_p)]
+                ("max_deg", ctypes.c_void_p), ("meta", ctypes.c_void_p), ("valid", ctypes.c_void_p),
+                ("unit_weights", ctypes.c_int32)]
 
 
 class Replay(ctypes.Structure):

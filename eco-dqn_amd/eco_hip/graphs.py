@@ -109,7 +109,7 @@ def edge_cap(kind, n, param, slack_sd=10.0):
 class GraphStore:
     """G graphs of N vertices resident on the device (eco_graph_set)."""
 
-    def __init__(self, row_ptr, edge_base, edges, device="cuda", stream=None):
+    def __init__(self, row_ptr, edge_base, edges, device="cuda", stream=None, unit_weights=None):
         dev = torch.device(device)
         self.device = dev
         if isinstance(row_ptr, torch.Tensor):
@@ -129,9 +129,13 @@ class GraphStore:
         self.max_deg = torch.zeros(self.n_graphs, dtype=torch.int32, device=dev)
         self.meta = torch.zeros(self.n_graphs, 4, dtype=torch.float64, device=dev)
         self.valid = torch.zeros(self.n_graphs, dtype=torch.int32, device=dev)
+        if unit_weights is None:  # every stored weight +-1: the dense-aggregation MPNN path applies
+            w = (self.edges.view(torch.int32) >> 24).to(torch.int8)
+            unit_weights = bool((w.abs() == 1).all().item()) if self.edges.numel() > 1 else True
+        self.unit_weights = bool(unit_weights)
         self.gs = _lib.GraphSet(self.n_graphs, self.n_spins, self.row_ptr.data_ptr(), self.edge_base.data_ptr(),
                                 self.edges.data_ptr(), self.deg.data_ptr(), self.max_deg.data_ptr(),
-                                self.meta.data_ptr(), self.valid.data_ptr())
+                                self.meta.data_ptr(), self.valid.data_ptr(), int(self.unit_weights))
         _lib.check(_lib.lib.eco_graphs_prepare(ctypes.byref(self.gs), _lib.stream_ptr(stream)))
 
     @classmethod
@@ -141,7 +145,7 @@ class GraphStore:
         rp = torch.zeros(n_graphs, n + 1, dtype=torch.int32, device=dev)
         eb = torch.arange(n_graphs, dtype=torch.int64, device=dev) * int(cap)
         ed = torch.zeros(max(1, n_graphs * int(cap)), dtype=torch.int32, device=dev)
-        st = cls(rp, eb, ed, device=dev)
+        st = cls(rp, eb, ed, device=dev, unit_weights=True)  # eco_graphs_generate writes +-1 / 1 weights
         st.cap = int(cap)
         return st
 

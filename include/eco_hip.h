@@ -93,6 +93,9 @@ typedef struct {
   int32_t *max_deg;         /* [G] max over rows of max(deg,1) */
   double *meta;             /* [G][4]: max_local_reward, quality_normalizer, lower_bound, sum(J) */
   int32_t *valid;           /* [G] 1 if the graph has a nonzero local reward */
+  int32_t unit_weights;     /* caller: 1 if every stored weight is +-1 (EdgeType.DISCRETE / UNIFORM graphs).
+                               Enables the dense-aggregation MPNN kernels for blocks of <= 224 rows; they
+                               verify it and report ECO_ERR_GRAPH through eco_check_errors if it is false. */
 } eco_graph_set;
 
 /* Graph metadata: MaximumCutUnbiasedScorer normalisers (score_solver.py:347-375)
