@@ -12,6 +12,7 @@ void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
 int32_t* err_word();  // device error word shared by all async kernels (eco_check_errors)
+int graphs_prepare_range(eco_graph_set* gs, int first, int count, hipStream_t st);  // eco_env.hip
 
 // ---- edge packing: column | (uint8 weight << 24) ----
 __device__ __forceinline__ int edge_col(uint32_t e) { return (int)(e & 0xFFFFFFu); }

@@ -11,15 +11,16 @@
 // f64 observation values are produced by the same IEEE operations as the
 // reference, so rewards/observations match it bit for bit.
 #include "eco_common.h"
+#include "eco_mpnn.h"
 
 namespace eco {
 
 // ------------------------------------------------------------------ graphs ----
 // score_solver.py:347-375 (normalisers) and mpnn.py:34-38 (degree norm).
-__global__ __launch_bounds__(256) void graphs_prepare_kernel(eco_graph_set gs) {
+__global__ __launch_bounds__(256) void graphs_prepare_kernel(eco_graph_set gs, int first, int count) {
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= gs.n_graphs) return;
+  const int g = first + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= first + count) return;
   const int N = gs.n_spins;
   const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
   const uint32_t* ed = gs.edges + gs.edge_base[g];
@@ -532,13 +533,26 @@ static int check_err_word(int32_t* w, hipStream_t st) {
 
 using namespace eco;
 
-extern "C" int eco_graphs_prepare(eco_graph_set* gs, eco_stream_t stream) {
+int eco::graphs_prepare_range(eco_graph_set* gs, int first, int count, hipStream_t st) {
   if (!gs || !gs->row_ptr || !gs->edge_base || !gs->edges || !gs->deg || !gs->max_deg || !gs->meta || !gs->valid)
     return fail(ECO_ERR_ARG, "incomplete graph set");
   if (gs->n_graphs < 1 || gs->n_spins < 1) return fail(ECO_ERR_ARG, "empty graph set");
-  const int blocks = (gs->n_graphs + 3) / 4;
-  graphs_prepare_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*gs);
-  return check_launch("graphs_prepare");
+  if (first < 0 || count < 1 || first + count > gs->n_graphs) return fail(ECO_ERR_ARG, "graph range out of set");
+  graphs_prepare_kernel<<<(count + 3) / 4, 256, 0, st>>>(*gs, first, count);
+  int rc = check_launch("graphs_prepare");
+  if (rc) return rc;
+  if (gs->adjbits && gs->unit_weights && adjbits_applies(gs->n_spins)) return adjbits_build(gs, first, count, st);
+  return ECO_OK;
+}
+
+extern "C" int eco_graphs_prepare(eco_graph_set* gs, eco_stream_t stream) {
+  if (!gs) return fail(ECO_ERR_ARG, "incomplete graph set");
+  return graphs_prepare_range(gs, 0, gs->n_graphs, (hipStream_t)stream);
+}
+
+extern "C" size_t eco_graphs_adjbits_bytes(int32_t n_spins, int32_t n_graphs) {
+  if (n_graphs < 1 || !adjbits_applies(n_spins)) return 0;
+  return (size_t)n_graphs * n_spins * 64;
 }
 
 extern "C" size_t eco_env_state_bytes(const eco_env_config* cfg, int32_t batch) {

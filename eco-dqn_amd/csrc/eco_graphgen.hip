@@ -215,7 +215,7 @@ extern "C" int eco_graphs_generate(eco_graph_set* gs, int32_t first, int32_t cou
   }
   int rc = check_launch("graphs_generate");
   if (rc) return rc;
-  return eco_graphs_prepare(gs, stream);
+  return graphs_prepare_range(gs, first, count, st);
 }
 
 extern "C" size_t eco_graphs_generate_workspace_bytes(int32_t n_spins, int32_t count) {

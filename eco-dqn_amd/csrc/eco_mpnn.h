@@ -91,6 +91,10 @@ enum { GR_DUU0 = 0, GR_DUU1, GR_DUU2, GR_DUM0, GR_DUM1, GR_DUM2, GR_DUE, GR_DU0,
 // whole graphs per workgroup block: up to 208 rows (13 tiles) share the LDS-resident embeddings
 inline int graphs_per_block(int N) { return N >= 208 ? 1 : 208 / N; }
 
+// dense-path bitmask adjacency of graphs [first, first + count) into gs->adjbits (eco_mpnn_dense.h)
+int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st);
+inline bool adjbits_applies(int n_spins) { return n_spins > 104 && n_spins <= 224; }
+
 size_t mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch);
 int mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_graph_set* gs, const int32_t* graph_ids,
                          int32_t batch, const float* obs_x, const void* saved, const float* dq, void* gradws,

@@ -187,6 +187,42 @@ __device__ __forceinline__ void glds_frags(uint16_t* dst, const uint16_t* src, i
 }
 __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Bitmask adjacency operand of one graph per workgroup (eco_graphs_prepare, 104 < N <= 224):
+// adjbits[g][v][q][k] = adj_bits16 of chunks 2k (low half) and 2k+1 (high half) for node v, lane quarter q.
+__global__ __launch_bounds__(256) void adjbits_kernel(eco_graph_set gs, int first) {
+  __shared__ uint32_t bm[DN_MAX_ROWS * DN_ADJW];
+  const int g = first + blockIdx.x;
+  const int N = gs.n_spins;
+  for (int i = threadIdx.x; i < N * DN_ADJW; i += 256) bm[i] = 0u;
+  __syncthreads();
+  const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
+  const uint32_t* ed = gs.edges + gs.edge_base[g];
+  for (int i = threadIdx.x; i < N * 4; i += 256) {
+    const int v = i >> 2;
+    for (int e = rp[v] + (i & 3); e < rp[v + 1]; e += 4) {
+      const uint32_t ex = ed[e];
+      const int j = edge_col(ex);
+      atomicOr(&bm[v * DN_ADJW + 2 * (j >> 5)], 1u << (j & 31));
+      if (edge_w(ex) < 0) atomicOr(&bm[v * DN_ADJW + 2 * (j >> 5) + 1], 1u << (j & 31));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N * 4; i += 256) {
+    const int v = i >> 2, q = i & 3;
+    const uint2* row = reinterpret_cast<const uint2*>(bm + v * DN_ADJW);
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = adj_bits16(row[2 * k], q) | (2 * k + 1 < DN_KC ? adj_bits16(row[2 * k + 1], q) << 16 : 0u);
+    *reinterpret_cast<uint4*>(gs.adjbits + (((size_t)g * N + v) * 4 + q) * 4) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st) {
+  adjbits_kernel<<<count, 256, 0, st>>>(*gs, first);
+  return check_launch("graphs_adjbits");
+}
+
 // LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
 //      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
 //      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
@@ -238,12 +274,14 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
     GB[gl] = a.gs.edge_base[gid];
     MD[gl] = a.gs.max_deg[gid];
   }
-  for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
+  const bool pre = a.gpb == 1 && a.gs.adjbits != nullptr;  // prepared bitmask operand (eco_graphs_prepare)
+  if (!pre)
+    for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
   __syncthreads();
   ECO_TS(1);
 
   // ---- adjacency bitmask (4 threads per row, 8 edge loads in flight per thread) ----
-  for (int i = threadIdx.x; i < rows_pad * 4; i += NT) {
+  for (int i = threadIdx.x; !pre && i < rows_pad * 4; i += NT) {
     const int r = i >> 2;
     if (r >= rows_valid) continue;
     const RowInfo ri = row_info(RI, r);
@@ -277,7 +315,11 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
   uint32_t adjb[4];
-  {
+  if (pre) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)a.gids[blk] * N + r) * 4 + s4) * 4);
+    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
+  } else {
     const uint2* arow = reinterpret_cast<const uint2*>(ADJ + rr * DN_ADJW);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -285,8 +327,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
       const uint32_t hi = 2 * k + 1 < DN_KC ? adj_bits16(arow[2 * k + 1], s4) : 0u;
       adjb[k] = lo | (hi << 16);
     }
+    __syncthreads();  // bitmask region free for the planes
   }
-  __syncthreads();  // bitmask region free for the planes
 
   // ---- phase A: Z[j][f] = Wx[f] . x_j (weights uniform over the wave); U = relu(Z + w_a) planes ----
   auto zval = [&](int f) {  // the CSR path's phase-A expression

@@ -38,7 +38,7 @@ class GraphSet(ctypes.Structure):
     _fields_ = [("n_graphs", ctypes.c_int32), ("n_spins", ctypes.c_int32), ("row_ptr", ctypes.c_void_p),
                 ("edge_base", ctypes.c_void_p), ("edges", ctypes.c_void_p), ("deg", ctypes.c_void_p),
                 ("max_deg", ctypes.c_void_p), ("meta", ctypes.c_void_p), ("valid", ctypes.c_void_p),
-                ("unit_weights", ctypes.c_int32)]
+                ("unit_weights", ctypes.c_int32), ("adjbits", ctypes.c_void_p)]
 
 
 class Replay(ctypes.Structure):
@@ -56,6 +56,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int32
 _SIG = {
     "eco_graphs_prepare": (ctypes.c_int, [ctypes.POINTER(GraphSet), _P]),
+    "eco_graphs_adjbits_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_graphs_generate_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_graphs_generate": (ctypes.c_int, [ctypes.POINTER(GraphSet), _I, _I, _I, ctypes.c_double, _I,
                                            ctypes.c_uint64, ctypes.c_int64, _P, _P]),

@@ -133,9 +133,13 @@ class GraphStore:
             w = (self.edges.view(torch.int32) >> 24).to(torch.int8)
             unit_weights = bool((w.abs() == 1).all().item()) if self.edges.numel() > 1 else True
         self.unit_weights = bool(unit_weights)
+        # dense-MPNN bitmask operand, built by eco_graphs_prepare (one graph per workgroup sizes only)
+        nb = _lib.lib.eco_graphs_adjbits_bytes(self.n_spins, self.n_graphs) if self.unit_weights else 0
+        self.adjbits = torch.zeros(nb // 4, dtype=torch.int32, device=dev) if nb else None
         self.gs = _lib.GraphSet(self.n_graphs, self.n_spins, self.row_ptr.data_ptr(), self.edge_base.data_ptr(),
                                 self.edges.data_ptr(), self.deg.data_ptr(), self.max_deg.data_ptr(),
-                                self.meta.data_ptr(), self.valid.data_ptr(), int(self.unit_weights))
+                                self.meta.data_ptr(), self.valid.data_ptr(), int(self.unit_weights),
+                                self.adjbits.data_ptr() if nb else None)
         _lib.check(_lib.lib.eco_graphs_prepare(ctypes.byref(self.gs), _lib.stream_ptr(stream)))
 
     @classmethod

@@ -96,11 +96,18 @@ typedef struct {
   int32_t unit_weights;     /* caller: 1 if every stored weight is +-1 (EdgeType.DISCRETE / UNIFORM graphs).
                                Enables the dense-aggregation MPNN kernels for blocks of <= 224 rows; they
                                verify it and report ECO_ERR_GRAPH through eco_check_errors if it is false. */
+  uint32_t *adjbits;        /* caller-allocated (eco_graphs_adjbits_bytes) or NULL; filled by eco_graphs_prepare:
+                               per graph, node and lane quarter the bitmask adjacency operand of the dense MPNN
+                               kernels ([G][N][4][4] u32), so they skip the per-call CSR -> bitmask build */
 } eco_graph_set;
 
 /* Graph metadata: MaximumCutUnbiasedScorer normalisers (score_solver.py:347-375)
  * and the MPNN degree normalisation (mpnn.py:34-38), computed on the device. */
 int eco_graphs_prepare(eco_graph_set *gs, eco_stream_t stream);
+
+/* Bytes of gs->adjbits for G graphs of N vertices: nonzero only where the dense MPNN path runs one graph
+ * per workgroup (104 < N <= 224); 0 means pass adjbits = NULL. */
+size_t eco_graphs_adjbits_bytes(int32_t n_spins, int32_t n_graphs);
 
 /* On-device graph generation into graphs [first, first+count) of a set whose edge slots are
  * fixed (edge_base[g] = g * edge_cap): the training-reset graph draws of
