@@ -35,7 +35,12 @@ constexpr int BF_HALF = 3 * 4 * 2 * BF_FRAG;         // one 64-input half of a L
 constexpr int BF_WF = 0;                             // edge_feature_NN: 1 half
 constexpr int BF_LAYER = BF_HALF;                    // + l * BF_LAYER_STRIDE: message (2 halves), then update
 constexpr int BF_LAYER_STRIDE = 4 * BF_HALF;
-constexpr int BF_TOTAL = BF_LAYER + 3 * BF_LAYER_STRIDE;  // bf16 elements
+constexpr int BF_FWD_END = BF_LAYER + 3 * BF_LAYER_STRIDE;
+// transposed Linears of the dense backward (y = W^T x: 64 inputs = forward outputs, forward inputs as
+// outputs in halves of 64): fragments [out half][p][nt][kc2], lane l: row 64 half + 16nt + (l&15) of W^T
+constexpr int BFT_WF = BF_FWD_END;                   // Wf^T: 1 half
+constexpr int BFT_LAYER = BFT_WF + BF_HALF;          // + l * BF_LAYER_STRIDE: Wm^T (2 halves), then Wu^T
+constexpr int BF_TOTAL = BFT_LAYER + 3 * BF_LAYER_STRIDE;  // bf16 elements
 constexpr int PK_TOTAL = PK_BF + BF_TOTAL / 2;
 
 // k' -> input feature of the bf16 Linear operands: within each 64-feature block, k' = 32kc + 8q + j

@@ -83,12 +83,14 @@ __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __rest
       const int e = 2 * (i - PK_BF) + t;
       const float* W;
       int in_dim, lin;
-      if (e < BF_LAYER) {
+      const bool tr = e >= BF_FWD_END;  // transposed fragments of the backward
+      const int et = tr ? e - BF_FWD_END : e;
+      if (et < BF_LAYER) {
         W = f + o.Wf;
         in_dim = 64;
-        lin = e;
+        lin = et;
       } else {
-        const int e2 = e - BF_LAYER;
+        const int e2 = et - BF_LAYER;
         const int l = e2 / BF_LAYER_STRIDE, r = e2 % BF_LAYER_STRIDE;
         W = f + o.L + l * 16384 + (r / (2 * BF_HALF)) * 8192;
         in_dim = 128;
@@ -98,7 +100,9 @@ __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __rest
       const int ln = within >> 3, jj = within & 7;
       const int kc2 = frag & 1, nt = (frag >> 1) & 3, pl = (frag >> 3) % 3, half = frag / 24;
       const int kp = 64 * half + 32 * kc2 + 8 * (ln >> 4) + jj;
-      const float wv = W[(16 * nt + (ln & 15)) * in_dim + bf16_kprime_feature(kp)];
+      // forward: W[16nt + (l&15)][feature(kp)];  transposed: W^T[64 half + 16nt + (l&15)][feature(kp & 63)]
+      const float wv = tr ? W[bf16_kprime_feature(kp & 63) * in_dim + 64 * half + 16 * nt + (ln & 15)]
+                          : W[(16 * nt + (ln & 15)) * in_dim + bf16_kprime_feature(kp)];
       uint16_t p1, p2, p3;
       split3_bits(wv, p1, p2, p3);
       h[t] = pl == 0 ? p1 : (pl == 1 ? p2 : p3);
@@ -892,6 +896,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.sv = (float*)saved;
   a.dq = dq;
   a.gr = (float*)gradws;
+  if (dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dense_launch(a, st);
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");

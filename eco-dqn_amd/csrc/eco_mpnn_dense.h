@@ -177,6 +177,48 @@ __device__ __forceinline__ void mm_bf3(f32x4 (&acc)[4], const float4 (&x)[4], co
   }
 }
 
+// Two output halves (fragment sets WH0, WH1) of one 64-input transposed Linear, sharing the split of x.
+__device__ __forceinline__ void mm_bf3x2(f32x4 (&acc0)[4], f32x4 (&acc1)[4], const float4 (&x)[4],
+                                         const uint16_t* WH0, const uint16_t* WH1, int lane) {
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    bf16x8 x1, x2, x3;
+    split_frag(x[2 * kc2], x[2 * kc2 + 1], x1, x2, x3);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint16_t* wl = (hh ? WH1 : WH0) + lane * 8;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4& acc = hh ? acc1[nt] : acc0[nt];
+        const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * BF_FRAG);
+        const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * BF_FRAG);
+        const bf16x8 w3 = *reinterpret_cast<const bf16x8*>(wl + ((2 * 4 + nt) * 2 + kc2) * BF_FRAG);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3, x1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x2, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x3, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x2, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight (register pressure at 16 waves)
+      }
+    }
+  }
+}
+
+// bit 4c + i: v[c] component i > 0
+__device__ __forceinline__ uint32_t pos_mask(const float4 (&v)[4]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    m |= (v[c].x > 0.f ? 1u : 0u) << (4 * c) | (v[c].y > 0.f ? 1u : 0u) << (4 * c + 1) |
+         (v[c].z > 0.f ? 1u : 0u) << (4 * c + 2) | (v[c].w > 0.f ? 1u : 0u) << (4 * c + 3);
+  return m;
+}
+__device__ __forceinline__ float4 masked(const f32x4& v, uint32_t m, int c) {
+  return make_float4((m >> (4 * c)) & 1u ? v[0] : 0.f, (m >> (4 * c + 1)) & 1u ? v[1] : 0.f,
+                     (m >> (4 * c + 2)) & 1u ? v[2] : 0.f, (m >> (4 * c + 3)) & 1u ? v[3] : 0.f);
+}
+
 // LDS-DMA copy of n_frag 1-KB weight fragments (global -> LDS, both contiguous, no registers):
 // wave w issues fragments w, w + NW, ...  Retire with glds_wait() before the barrier that publishes them.
 template <int NW>
@@ -223,6 +265,56 @@ int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st)
   return check_launch("graphs_adjbits");
 }
 
+// The lane's adjacency operand (adj_bits16 of every k-chunk, packed in 4 words): read from the prepared
+// gs.adjbits when the block holds one graph, else built here from the CSR rows in ADJ (LDS scratch of
+// rows_pad * DN_ADJW words, free again on return).  RI and GB must be staged (and a barrier passed).
+template <int NT>
+__device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ, const int2* RI, const int64_t* GB,
+                                                int blk, int rows_pad, int rows_valid, int r, int rr, bool valid,
+                                                int s4, uint32_t (&adjb)[4]) {
+  const int N = a.N;
+  if (a.gpb == 1 && a.gs.adjbits != nullptr) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)a.gids[blk] * N + r) * 4 + s4) * 4);
+    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
+    return;
+  }
+  for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
+  __syncthreads();
+  // 4 threads per row, 8 edge loads in flight per thread
+  for (int i = threadIdx.x; i < rows_pad * 4; i += NT) {
+    const int row = i >> 2;
+    if (row >= rows_valid) continue;
+    const RowInfo ri = row_info(RI, row);
+    const int base = (row / N) * N;
+    const uint32_t* eg = a.gs.edges + GB[row / N];
+    for (int e = ri.e0 + (i & 3); e < ri.e1; e += 32) {
+      uint32_t ex[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ex[k] = e + 4 * k < ri.e1 ? eg[e + 4 * k] : 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (e + 4 * k >= ri.e1) break;
+        const int j = base + edge_col(ex[k]);
+        const int wv = edge_w(ex[k]);
+        if (wv != 1 && wv != -1) atomicCAS(a.err, 0, ECO_ERR_GRAPH);  // the caller's unit_weights was wrong
+        uint32_t* word = ADJ + row * DN_ADJW + 2 * (j >> 5);
+        atomicOr(word, 1u << (j & 31));
+        if (wv < 0) atomicOr(word + 1, 1u << (j & 31));
+      }
+    }
+  }
+  __syncthreads();
+  const uint2* arow = reinterpret_cast<const uint2*>(ADJ + rr * DN_ADJW);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t lo = adj_bits16(arow[2 * k], s4);
+    const uint32_t hi = 2 * k + 1 < DN_KC ? adj_bits16(arow[2 * k + 1], s4) : 0u;
+    adjb[k] = lo | (hi << 16);
+  }
+  __syncthreads();
+}
+
 // LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
 //      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
 //      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
@@ -254,7 +346,6 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const uint16_t* PB = reinterpret_cast<const uint16_t*>(P + PK_BF);
   const int s4 = lane >> 4;
   const int c16 = lane & 15;
-  const uint32_t* __restrict__ edges = a.gs.edges;
 
   // plane-mapped role (phases A-C): row j = 64 (w & 3) + lane, features 16 (w >> 2) .. +15
   const int pj = 64 * (w & 3) + lane;
@@ -274,37 +365,9 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
     GB[gl] = a.gs.edge_base[gid];
     MD[gl] = a.gs.max_deg[gid];
   }
-  const bool pre = a.gpb == 1 && a.gs.adjbits != nullptr;  // prepared bitmask operand (eco_graphs_prepare)
-  if (!pre)
-    for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
   __syncthreads();
   ECO_TS(1);
-
-  // ---- adjacency bitmask (4 threads per row, 8 edge loads in flight per thread) ----
-  for (int i = threadIdx.x; !pre && i < rows_pad * 4; i += NT) {
-    const int r = i >> 2;
-    if (r >= rows_valid) continue;
-    const RowInfo ri = row_info(RI, r);
-    const int base = (r / N) * N;
-    const uint32_t* eg = edges + GB[r / N];
-    for (int e = ri.e0 + (i & 3); e < ri.e1; e += 32) {
-      uint32_t ex[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ex[k] = e + 4 * k < ri.e1 ? eg[e + 4 * k] : 0u;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (e + 4 * k >= ri.e1) break;
-        const int j = base + edge_col(ex[k]);
-        const int wv = edge_w(ex[k]);
-        if (wv != 1 && wv != -1) atomicCAS(a.err, 0, ECO_ERR_GRAPH);  // the caller's unit_weights was wrong
-        uint32_t* word = ADJ + r * DN_ADJW + 2 * (j >> 5);
-        atomicOr(word, 1u << (j & 31));
-        if (wv < 0) atomicOr(word + 1, 1u << (j & 31));
-      }
-    }
-  }
-  __syncthreads();
-  // this lane's node and its k-chunk range; its adjacency bits move to registers
+  // this lane's node and its k-chunk range; its adjacency bits in registers
   const bool has_tile = w < ntiles;
   const int r = w * 16 + c16;
   const bool valid = has_tile && r < rows_valid;
@@ -315,20 +378,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
   uint32_t adjb[4];
-  if (pre) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)a.gids[blk] * N + r) * 4 + s4) * 4);
-    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
-  } else {
-    const uint2* arow = reinterpret_cast<const uint2*>(ADJ + rr * DN_ADJW);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t lo = adj_bits16(arow[2 * k], s4);
-      const uint32_t hi = 2 * k + 1 < DN_KC ? adj_bits16(arow[2 * k + 1], s4) : 0u;
-      adjb[k] = lo | (hi << 16);
-    }
-    __syncthreads();  // bitmask region free for the planes
-  }
+  dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
 
   // ---- phase A: Z[j][f] = Wx[f] . x_j (weights uniform over the wave); U = relu(Z + w_a) planes ----
   auto zval = [&](int f) {  // the CSR path's phase-A expression
@@ -505,6 +555,318 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= DN_WP_BYTES;
   readout_act<SAVE, NW>(a, Hs, LDH, Scr, split, blk, g_valid, rows_valid, R0, RT);
   ECO_TS(8);
+}
+
+// ============================================================== backward ====
+// Autograd of mpnn_forward_dense_kernel (dqn.py:440-449) for the same blocks: every A^T product is the
+// dense aggregation of the forward (A symmetric), every Linear a transposed bf16x3 product (BFT_*
+// fragments).  Writes the pre-activation gradients the weight-gradient reduction reads (GR_DUU*, GR_DUM*,
+// GR_DUE, GR_DU0, GR_DZ) and the per-graph / per-block partials of the CSR backward; dh and de stay in
+// registers (no GR_DE / GR_DH round trips).
+// LDS: PL planes of the gathered gradient G (readout scratch first) | WP 48 fragments | WX 24 fragments |
+//      RI [rows_pad] int2 | GB [gpb] i64
+__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense_kernel(MpnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(16);
+  constexpr int NW = DN_NW;
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);
+  uint16_t* WP = PL + 3 * DN_PLANE;
+  uint16_t* WX = WP + 2 * BF_HALF;
+  int2* RI = reinterpret_cast<int2*>(WX + BF_HALF);
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PB = reinterpret_cast<const uint16_t*>(P + PK_BF);
+  const float* sv = a.sv;
+  float* gr = a.gr;
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
+  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
+  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
+  const float* PP = MEAN + (size_t)a.B * 64;
+  float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
+  float* DWRA = DP + (size_t)a.B * 64;
+  float* DWRB = DWRA + (size_t)a.B * 64;
+  float* DBR = DWRB + (size_t)a.B * 64;
+  float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
+
+  // ---- staging: layer-2 transposed weights (LDS-DMA), row info, edge bases ----
+  glds_frags<NW>(WP, PB + BFT_LAYER + 2 * BF_LAYER_STRIDE + 2 * BF_HALF, 48, w, lane);  // Wu^T
+  glds_frags<NW>(WX, PB + BFT_LAYER + 2 * BF_LAYER_STRIDE, 24, w, lane);                // Wm^T (dagg half)
+  for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
+  __syncthreads();
+  const bool has_tile = w < ntiles;
+  const int r = w * 16 + c16;
+  const bool valid = has_tile && r < rows_valid;
+  const int rr = min(r, rows_pad - 1);
+  const RowInfo ri = row_info(RI, rr);
+  const float nf = (float)ri.norm;
+  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  uint32_t adjb[4];
+  dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
+  ECO_TS(17);
+
+  // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
+  float* DQ = lds;                       // [rows_pad]
+  float* DMEAN = DQ + rows_pad;          // [gpb][64]
+  float* RED = DMEAN + a.gpb * 64;       // [gpb][NW][64] (split) or [NW][64]
+  const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)DN_PL_BYTES;
+  for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
+  __syncthreads();
+  if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
+    for (int gl = 0; gl < g_valid; ++gl) {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      float dwb = 0.f;
+      for (int v = w; v < N; v += NW) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+      RED[(gl * NW + w) * 64 + lane] = dwb;
+    }
+    __syncthreads();
+  }
+  for (int gl = w; gl < g_valid; gl += NW) {
+    const int e = blk * a.gpb + gl;
+    float sacc = 0.f;
+    for (int v = lane; v < N; v += 64) sacc += DQ[gl * N + v];
+    const float S = wave_sum_f(sacc);
+    const float p = PP[(size_t)e * 64 + lane];
+    const float dp = P[PK_WR + lane] * S * (p > 0.f ? 1.f : 0.f);
+    DP[(size_t)e * 64 + lane] = dp;
+    DWRA[(size_t)e * 64 + lane] = relu(p) * S;
+    if (lane == 0) DBR[e] = S;
+    float dmean = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
+    DMEAN[gl * 64 + lane] = dmean / (float)N;
+    float dwb = 0.f;
+    if (split) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) dwb += RED[(gl * NW + k) * 64 + lane];  // fixed order
+    } else {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      for (int v = 0; v < N; ++v) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+    }
+    DWRB[(size_t)e * 64 + lane] = dwb;
+  }
+  __syncthreads();
+  // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
+  float4 dh[4];
+  {
+    const float dqi = valid ? DQ[r] : 0.f;
+    const int gl = rr / N;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 16 * c + 4 * s4;
+      const float4 dm = valid ? f4(DMEAN + gl * 64 + f) : zero4();
+      dh[c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
+                          fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
+    }
+  }
+  __syncthreads();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes (0 * garbage = NaN)
+  {
+    const int KP = (rows_pad + 31) & ~31;
+    const int pad = KP - rows_pad;  // 0 or 16 rows
+    for (int i = threadIdx.x; i < 3 * 4 * pad * 8; i += NT) {  // 8 dwords per 32-B row
+      const int pf = i / (pad * 8), rem = i - pf * (pad * 8);
+      reinterpret_cast<uint32_t*>(PL + (pf >> 2) * DN_PLANE + (pf & 3) * (DN_KPMAX * 16) + rows_pad * 16)[rem] = 0u;
+    }
+  }
+  ECO_TS(18);
+
+  // ---- update layers in reverse (mpnn.py:114-120) ----
+  // [B0: Wu^T in WP, Wm^T(dagg half) in WX; planes free] dh_direct, dm | [B1] DMA Wm^T(de half) -> WP;
+  // dagg -> G planes | [B2] de; DMA next Wm^T(dagg half) -> WX; dh = dh_direct + A.G | [B3] DMA next Wu^T -> WP
+  float4 de[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) de[c] = zero4();
+  for (int layer = 2; layer >= 0; --layer) {
+    const uint16_t* WmT = PB + BFT_LAYER + layer * BF_LAYER_STRIDE;
+    const size_t ro = (R0 + rr) * 64 + 4 * s4;
+    // duu = dh' * [h' > 0]
+    float4 duu[4];
+    uint32_t mmask;
+    {
+      float4 hv[4], mv[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        hv[c] = valid ? f4(SV(SV_H0 + layer + 1) + ro + 16 * c) : zero4();
+        mv[c] = valid ? f4(SV(SV_M0 + layer) + ro + 16 * c) : zero4();
+      }
+      mmask = pos_mask(mv);
+      const uint32_t hmask = pos_mask(hv);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        duu[c] = masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, hmask, c);
+        if (valid) st4(GR(GR_DUU0 + layer) + ro + 16 * c, duu[c]);
+      }
+    }
+    glds_wait();
+    __syncthreads();  // B0
+    // [dh_direct, dm] = Wu^T . duu
+    f32x4 dhd[4], dmm[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      dhd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dmm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (has_tile) mm_bf3x2(dhd, dmm, duu, WP, WP + BF_HALF, lane);
+    // dum = dm * [m > 0]
+    float4 dum[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      dum[c] = masked(dmm[c], mmask, c);
+      if (valid) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
+    }
+    __syncthreads();  // B1: WP free
+    glds_frags<NW>(WP, WmT + BF_HALF, 24, w, lane);  // Wm^T, de half
+    // dagg = Wm^T(agg half) . dum;  G = dagg / norm (d agg / d(A.h) = 1/norm) -> planes
+    f32x4 dg[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) {
+      mm_bf3(dg, dum, WX, lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        plane_store4(PL, c, r, s4, valid ? make_float4(dg[c][0] / nf, dg[c][1] / nf, dg[c][2] / nf, dg[c][3] / nf)
+                                         : zero4());
+    }
+    glds_wait();
+    __syncthreads();  // B2: G planes complete, Wm^T de half landed, WX free
+    if (layer > 0) glds_frags<NW>(WX, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE, 24, w, lane);
+    else glds_frags<NW>(WX, PB + BFT_WF, 24, w, lane);  // Wf^T for the edge layer
+    f32x4 dd[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) mm_bf3(dd, dum, WP, lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      de[c].x += dd[c][0]; de[c].y += dd[c][1]; de[c].z += dd[c][2]; de[c].w += dd[c][3];
+    }
+    // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
+    f32x4 ag[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) ag[nt] = dhd[nt];
+    if (has_tile) dense_agg<0>(ag, PL, adjb, kc0, kc1, lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dh[c] = valid ? as_f4(ag[c]) : zero4();
+    __syncthreads();  // B3: WP and the planes free
+    if (layer > 0) glds_frags<NW>(WP, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE + 2 * BF_HALF, 48, w, lane);
+    ECO_TS(21 - layer);
+  }
+
+  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due ----
+  const size_t ro = (R0 + rr) * 64 + 4 * s4;
+  float4 due[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 hv = valid ? f4(SV(SV_H0) + ro + 16 * c) : zero4();
+    const float4 ev = valid ? f4(SV(SV_E) + ro + 16 * c) : zero4();
+    if (valid) {
+      st4(GR(GR_DU0) + ro + 16 * c, make_float4(hv.x > 0.f ? dh[c].x : 0.f, hv.y > 0.f ? dh[c].y : 0.f,
+                                                hv.z > 0.f ? dh[c].z : 0.f, hv.w > 0.f ? dh[c].w : 0.f));
+    }
+    due[c] = make_float4(ev.x > 0.f ? de[c].x : 0.f, ev.y > 0.f ? de[c].y : 0.f, ev.z > 0.f ? de[c].z : 0.f,
+                         ev.w > 0.f ? de[c].w : 0.f);
+    if (valid) st4(GR(GR_DUE) + ro + 16 * c, due[c]);
+  }
+  glds_wait();
+  __syncthreads();  // Wf^T landed
+  {
+    f32x4 dg[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) {
+      mm_bf3(dg, due, WX, lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        plane_store4(PL, c, r, s4, valid ? make_float4(dg[c][0] / nf, dg[c][1] / nf, dg[c][2] / nf, dg[c][3] / nf)
+                                         : zero4());
+    }
+  }
+  __syncthreads();
+  ECO_TS(22);
+  // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
+  {
+    f32x4 gp[4], gm[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      gp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (has_tile) {
+      dense_agg<1>(gp, PL, adjb, kc0, kc1, lane);
+      dense_agg<2>(gm, PL, adjb, kc0, kc1, lane);
+    }
+    float4 x0 = zero4(), x1 = zero4();
+    if (valid) {
+      x0 = f4(a.x + (R0 + r) * 8);
+      x1 = f4(a.x + (R0 + r) * 8 + 4);
+    }
+    __syncthreads();  // every wave is done reading the G planes: the region becomes the dwa scratch
+    float* REDW = lds;  // [NW][64]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float dz4[4], dwa4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * c + 4 * s4 + i;
+        const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
+        const float z = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
+                        w1.z * x1.z + w1.w * x1.w;
+        const float wa = P[PK_WA + f];
+        const float tp = fmaf(1.f, wa, z) > 0.f ? gp[c][i] : 0.f;
+        const float tm = fmaf(-1.f, wa, z) > 0.f ? gm[c][i] : 0.f;
+        dz4[i] = valid ? tp + tm : 0.f;
+        // reduce dw_a over the 16 node lanes sharing s4
+        float v = valid ? tp - tm : 0.f;
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        dwa4[i] = v;
+      }
+      if (valid) st4(GR(GR_DZ) + (R0 + r) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
+      if (c16 == 0) st4(REDW + w * 64 + 16 * c + 4 * s4, make_float4(dwa4[0], dwa4[1], dwa4[2], dwa4[3]));
+    }
+    __syncthreads();
+    if (w == 0) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) sacc += REDW[k * 64 + lane];
+      DWA[(size_t)blk * 64 + lane] = sacc;
+    }
+  }
+  ECO_TS(23);
+}
+
+static int mpnn_backward_dense_launch(const MpnnArgs& a, hipStream_t st) {
+  const int rows_pad = (a.gpb * a.N + 15) & ~15;
+  const size_t lds = dense_fwd_lds_bytes(rows_pad, a.gpb);
+  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  mpnn_backward_dense_kernel<<<blocks, 64 * DN_NW, lds, st>>>(a);
+  return check_launch("mpnn_backward_dense");
 }
 
 static int mpnn_forward_dense_launch(const MpnnArgs& a, bool save, hipStream_t st) {
