@@ -22,7 +22,7 @@ struct WJob {
   int out_col0;      // first column in the flat buffer
 };
 constexpr int MAX_JOBS = 10;
-constexpr int WG_PER_JOB = 64;
+constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
 constexpr int WROWS = 32;                  // rows per LDS tile
@@ -54,26 +54,51 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
-  for (int rb = r0; rb < r1; rb += WROWS) {
-    // stage dY [32][64] and X [32][K4]
-    for (int i = threadIdx.x; i < WROWS * 16; i += 256) {
+  // register double-buffering: tile rb + 32 is loaded while tile rb's MFMAs run
+  const int per = K4 >> 2;
+  float4 ry[2], rx[4];
+  auto load_tile = [&](int rb) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = threadIdx.x + 256 * k;  // WROWS * 16 = 512 float4
       const int r = i >> 4, c = (i & 15) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rb + r < r1) v = *reinterpret_cast<const float4*>(J.dY + (size_t)(rb + r) * 64 + c);
-      *reinterpret_cast<float4*>(sY + r * LDY + c) = v;
+      ry[k] = rb + r < r1 ? *reinterpret_cast<const float4*>(J.dY + (size_t)(rb + r) * 64 + c)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const int per = K4 >> 2;
-    for (int i = threadIdx.x; i < WROWS * per; i += 256) {
-      const int r = i / per, c = (i - r * per) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rb + r < r1) {
-        const size_t rr = (size_t)(rb + r);
-        v = c < J.K1 ? *reinterpret_cast<const float4*>(J.X1 + rr * J.ld1 + c)
-                     : *reinterpret_cast<const float4*>(J.X2 + rr * J.ld2 + (c - J.K1));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + 256 * k;  // up to WROWS * 32 = 1024 float4
+      rx[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < WROWS * per) {
+        const int r = i / per, c = (i - r * per) * 4;
+        if (rb + r < r1) {
+          const size_t rr = (size_t)(rb + r);
+          rx[k] = c < J.K1 ? *reinterpret_cast<const float4*>(J.X1 + rr * J.ld1 + c)
+                           : *reinterpret_cast<const float4*>(J.X2 + rr * J.ld2 + (c - J.K1));
+        }
       }
-      *reinterpret_cast<float4*>(sX + r * LDX + c) = v;
     }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      *reinterpret_cast<float4*>(sY + (i >> 4) * LDY + (i & 15) * 4) = ry[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < WROWS * per) {
+        const int r = i / per, c = (i - r * per) * 4;
+        *reinterpret_cast<float4*>(sX + r * LDX + c) = rx[k];
+      }
+    }
+  };
+  if (r0 < r1) load_tile(r0);
+  for (int rb = r0; rb < r1; rb += WROWS) {
+    store_tile();
     __syncthreads();
+    if (rb + WROWS < r1) load_tile(rb + WROWS);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int t = w + 4 * q;

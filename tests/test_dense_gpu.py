@@ -1,0 +1,117 @@
+"""The dense-aggregation MPNN kernels (eco_mpnn_dense.h: blocks of <= 224 rows, +-1 weights) against
+the CSR-gather kernels (eco_mpnn.hip) on the same inputs, and against the fp32 torch oracle.
+
+The CSR path is selected per call with ECO_MPNN_NO_DENSE=1.  Both compute the reference's fp32
+arithmetic in a different summation order (dense: exact bf16x3 splits, fp32 accumulation), so the bars
+are the oracle tolerances of test_mpnn_gpu / test_dqn_gpu:
+  Q: |q - q_ref| <= 5e-5 (1 + |q_ref|);  gradients: relative L2 error < 2e-4 per parameter tensor.
+Covers one graph per block with the prepared bitmask (N = 150, 200, 224), one graph per block built
+in-kernel (adjbits dropped), several graphs per block (N = 20, 64), padding rows, and the fallback for
+non-unit weights."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mpnn_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(n, B, seed, kind="ER", param=0.15):
+    from eco_hip.graphs import GraphStore
+    g = torch.Generator().manual_seed(seed)
+    w = mo.init_weights(g, std=0.1)
+    store = GraphStore.random(kind, B, n, param, seed=seed)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    dq = torch.randn(B, n, generator=g)
+    return w, store, x.cuda(), dq.cuda()
+
+
+def _run(net, store, x, dq, scope, dense):
+    from eco_hip.networks.mpnn import MPNN
+    B, n = x.shape[0], x.shape[1]
+    if dense:
+        os.environ.pop("ECO_MPNN_NO_DENSE", None)
+    else:
+        os.environ["ECO_MPNN_NO_DENSE"] = "1"
+    try:
+        gids = torch.arange(B, dtype=torch.int32, device="cuda")
+        q = net.forward_graphs(x, store, gids, norm_scope=scope).clone()
+        saved = torch.empty(MPNN.saved_bytes(n, B), dtype=torch.uint8, device="cuda")
+        qs = net.forward_graphs(x, store, gids, norm_scope=1, saved=saved).clone()
+        grad = torch.zeros_like(net.flat)
+        net.backward_graphs(x, store, gids, saved, dq, grad)
+        torch.cuda.synchronize()
+        return q.cpu(), qs.cpu(), grad.cpu()
+    finally:
+        os.environ.pop("ECO_MPNN_NO_DENSE", None)
+
+
+def _scaled_err(a, b):
+    return float(((a - b).abs() / (1 + b.abs())).max())
+
+
+@pytest.mark.parametrize("n,B,prepared", [(200, 24, True), (224, 9, True), (150, 16, True), (200, 10, False),
+                                          (20, 64, False), (64, 19, False)])
+def test_dense_matches_csr_and_oracle(n, B, prepared):
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_GRAPH
+    from test_dqn_gpu import _flat_to_dict
+    w, store, x, dq = _inputs(n, B, seed=n + B)
+    assert store.unit_weights
+    assert (store.adjbits is not None) == (104 < n <= 224)
+    if not prepared:  # force the in-kernel bitmask build
+        store.gs.adjbits = None
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    qd, qsd, gd = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=True)
+    qc, qsc, gc = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=False)
+    assert torch.isfinite(qd).all() and torch.isfinite(gd).all()
+    assert _scaled_err(qd, qc) <= 5e-5 and _scaled_err(qsd, qsc) <= 5e-5
+    for b in [0, B // 2, B - 1]:  # oracle, per-graph norm scope (B=1 semantics)
+        obs = torch.from_numpy(np.vstack([x[b, :, :7].cpu().numpy().T.astype(np.float64), store.dense(b)])).float()
+        assert _scaled_err(qd[b], mo.forward(w, obs)) <= 5e-5
+    # gradients: dense vs torch autograd of the oracle (norm.max over the batch, as train_step)
+    obs = torch.from_numpy(np.stack([np.vstack([x[b, :, :7].cpu().numpy().T.astype(np.float64), store.dense(b)])
+                                     for b in range(B)])).float()
+    wg = {k: v.clone().requires_grad_(True) for k, v in w.items()}
+    (mo.forward(wg, obs) * dq.cpu()).sum().backward()
+    dd, dc = _flat_to_dict(gd), _flat_to_dict(gc)
+    for k in mo.KEYS:
+        ref = wg[k].grad
+        err = float((dd[k] - ref).norm() / max(float(ref.norm()), 1e-12))
+        assert err < 2e-4, (k, err)
+        # CSR path: same math, other summation order; a ReLU input within rounding of 0 may take the other
+        # side (seen: one element of e at N=20), so this cross-check only catches gross errors
+        err_c = float((dd[k] - dc[k]).norm() / max(float(dc[k].norm()), 1e-12))
+        assert err_c < 2e-2, (k, err_c)
+
+
+def test_non_unit_weights_use_the_csr_path():
+    """Weights of +-2 are outside the dense kernels' {0, +-1} operand: the store says so and the forward
+    still matches the oracle (CSR gather)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    rng = np.random.default_rng(0)
+    n, B = 40, 6
+    mats = []
+    for _ in range(B):
+        a = np.triu((rng.random((n, n)) < 0.2) * rng.choice([-2.0, 1.0, 2.0], (n, n)), 1)
+        mats.append(a + a.T)
+    store = GraphStore.from_dense(mats)
+    assert not store.unit_weights and store.adjbits is None
+    g = torch.Generator().manual_seed(5)
+    w = mo.init_weights(g, std=0.1)
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g)
+    gids = torch.arange(B, dtype=torch.int32, device="cuda")
+    q = net.forward_graphs(x.cuda(), store, gids).cpu()
+    for b in range(B):
+        obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), mats[b]])).float()
+        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-5
