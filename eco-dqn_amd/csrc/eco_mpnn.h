@@ -8,6 +8,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int MPNN_MAX_SPINS = 512;  // block of one graph must fit LDS (rows_pad * 272 B + scratch)
+constexpr int MPNN_MAX_SPINS_LARGE = ECO_MAX_SPINS;  // global-memory embeddings (inference only) above 512
 constexpr int LDH = 72;              // LDS row stride (floats) of 64-wide tiles: = 8 (mod 64) makes the MFMA
                                      // operand reads (16 rows x 4 quads per ds_read_b128 lane group) conflict-free
 constexpr int LDW = 136;             // LDS row stride of staged [64][128] weights (same property)

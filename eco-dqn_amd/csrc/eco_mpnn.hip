@@ -727,6 +727,177 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
   ECO_TS(23);
 }
 
+// ======================================================== large graphs ====
+// N > 512 (GSet G22, N = 2000; inference / best-cut search only): the node embeddings no longer fit
+// LDS, so each episode's Z / h rows live in global memory (two ping-pong [rows][64] f32 buffers and the
+// edge embedding e, in the forward workspace: per episode 3 x rows x 256 B, L2/MALL-resident while the
+// workgroup runs).  One workgroup per episode; waves take 16-node tiles round-robin; the
+// aggregations are CSR gathers from global rows in the MFMA operand layout; the Linears are the same
+// exact-f32 MFMA tiles as the LDS kernels with both layer weights staged in LDS (8 waves: the gathers
+// and the 8-chunk Linears need more than the 128 VGPRs of a 16-wave workgroup).
+// LDS: Wl [2][64][LDW] | readout scratch
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs a, float* hbuf) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int e = blockIdx.x;
+  const int N = a.N;
+  const int rows_pad = (N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  const size_t R0 = (size_t)e * N;
+  const size_t RT = (size_t)a.B * N;
+  float* Wl = lds;
+  float* Scr = lds + 2 * 64 * LDW;
+  float* HA = hbuf + (size_t)e * rows_pad * 64 * 3;
+  float* HB = HA + (size_t)rows_pad * 64;
+  float* EB = HB + (size_t)rows_pad * 64;
+  const float* P = a.P;
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  const int gid = a.gids[e];
+  const uint32_t* __restrict__ eg = a.gs.edges + a.gs.edge_base[gid];
+  const float* x = a.x + R0 * 8;
+  auto rinfo = [&](int r) { return row_info_packed(pack_row_info(a, e, r, N)); };
+
+  // ---- phase A: Z = Wx . x into HB; Wf staged ----
+  stage_rows<NT>(Wl, LDH, P + PK_WF, 64, 64, 64);
+  {
+    float wx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wx[k] = P[PK_WX + lane * 8 + k];
+    for (int r = w; r < rows_pad; r += NW) {
+      float z = 0.f;
+      if (r < N) {
+        const float4 x0 = f4(x + r * 8), x1 = f4(x + r * 8 + 4);
+        z = wx[0] * x0.x + wx[1] * x0.y + wx[2] * x0.z + wx[3] * x0.w + wx[4] * x1.x + wx[5] * x1.y +
+            wx[6] * x1.z + wx[7] * x1.w;
+      }
+      HB[(size_t)r * 64 + lane] = z;
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // ---- phase B: edge embedding (mpnn.py:89-104) -> EB; phase C: h0 = relu(W0 . x) -> HA ----
+  {
+    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : a.gs.max_deg[gid];
+    float wa[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wa[c * 4 + i] = P[PK_WA + 16 * c + 4 * s4 + i];
+    for (int t = w; t < ntiles; t += NW) {
+      const int r = t * 16 + c16;
+      const bool valid = r < N;
+      const RowInfo ri = rinfo(r);
+      float4 acc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = zero4();
+      for_edges(eg, ri.e0, ri.e1, [&](uint32_t ex) {
+        const float wv = (float)edge_w(ex);
+        const float* zr = HB + (size_t)edge_col(ex) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 z = f4(zr + 16 * c);
+          acc[c].x += relu(fmaf(wv, wa[4 * c + 0], z.x));
+          acc[c].y += relu(fmaf(wv, wa[4 * c + 1], z.y));
+          acc[c].z += relu(fmaf(wv, wa[4 * c + 2], z.z));
+          acc[c].w += relu(fmaf(wv, wa[4 * c + 3], z.w));
+        }
+      });
+      const float nf = (float)ri.norm;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        acc[c].x = acc[c].x / nf; acc[c].y = acc[c].y / nf; acc[c].z = acc[c].z / nf; acc[c].w = acc[c].w / nf;
+      }
+      if (s4 == 3) acc[3].w = nf / (float)maxdeg_call;  // norm / norm.max() (mpnn.py:102)
+      if (!valid) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = zero4();
+      }
+      f32x4 d[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mm_k<4, 4, true>(d, acc, Wl, LDH, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) st4(EB + (size_t)r * 64 + 16 * nt + 4 * s4, relu4(d[nt]));
+    }
+    float w0[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w0[k] = P[PK_W0 + lane * 8 + k];
+    for (int r = w; r < rows_pad; r += NW) {
+      float h0 = 0.f;
+      if (r < N) {
+        const float4 x0 = f4(x + r * 8), x1 = f4(x + r * 8 + 4);
+        h0 = relu(w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x + w0[5] * x1.y +
+                  w0[6] * x1.z + w0[7] * x1.w);
+      }
+      HA[(size_t)r * 64 + lane] = h0;
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120), HA <-> HB ----
+  float* Hc = HA;
+  float* Hn = HB;
+  for (int layer = 0; layer < 3; ++layer) {
+    const float* Wm = P + PK_LAYER + layer * 16384;
+    stage_rows<NT>(Wl, LDW, Wm, 128, 64, 128);
+    stage_rows<NT>(Wl + 64 * LDW, LDW, Wm + 8192, 128, 64, 128);
+    __syncthreads();
+    for (int t = w; t < ntiles; t += NW) {
+      const int r = t * 16 + c16;
+      const bool valid = r < N;
+      const RowInfo ri = rinfo(r);
+      float4 am[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) am[c] = zero4();
+      for_edges(eg, ri.e0, ri.e1, [&](uint32_t ex) {
+        const float wv = (float)edge_w(ex);
+        const float* hr = Hc + (size_t)edge_col(ex) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 hv = f4(hr + 16 * c);
+          am[c].x = fmaf(wv, hv.x, am[c].x);
+          am[c].y = fmaf(wv, hv.y, am[c].y);
+          am[c].z = fmaf(wv, hv.z, am[c].z);
+          am[c].w = fmaf(wv, hv.w, am[c].w);
+        }
+      });
+      const float nf = (float)ri.norm;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        am[c].x = am[c].x / nf; am[c].y = am[c].y / nf; am[c].z = am[c].z / nf; am[c].w = am[c].w / nf;
+        am[4 + c] = f4(EB + (size_t)r * 64 + 16 * c + 4 * s4);
+      }
+      f32x4 d[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mm_k<4, 8, true>(d, am, Wl, LDW, lane);
+      float4 au[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        au[c] = f4(Hc + (size_t)r * 64 + 16 * c + 4 * s4);
+        au[4 + c] = relu4(d[c]);
+      }
+      f32x4 hn[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mm_k<4, 8, true>(hn, au, Wl + 64 * LDW, LDW, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) st4(Hn + (size_t)r * 64 + 16 * nt + 4 * s4, valid ? relu4(hn[nt]) : zero4());
+    }
+    __threadfence();  // release the Hn rows and invalidate this CU's L1 before other waves read them
+    __syncthreads();  // every wave done with Hc, Wl; Hn complete
+    float* tmp = Hc;
+    Hc = Hn;
+    Hn = tmp;
+  }
+  // ---- phase E: readout + act over the h3 rows in global memory ----
+  readout_act<false, NW>(a, Hc, 64, Scr, true, e, 1, N, R0, RT);
+}
+
 __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, int B, int* out) {
   int m = 1;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) m = max(m, gs.max_deg[gids[i]]);
@@ -740,7 +911,7 @@ static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco
   if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
   if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
   const int N = gs->n_spins;
-  if (N < 1 || N > MPNN_MAX_SPINS) return fail(ECO_ERR_ARG, "mpnn supports 1 <= N <= 512");
+  if (N < 1 || N > MPNN_MAX_SPINS_LARGE) return fail(ECO_ERR_ARG, "mpnn supports 1 <= N <= 2048");
   if (norm_scope != ECO_NORM_PER_GRAPH && norm_scope != ECO_NORM_PER_CALL)
     return fail(ECO_ERR_ARG, "bad norm_scope");
   a = MpnnArgs{};
@@ -777,6 +948,8 @@ extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packe
 
 extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
   if (n_spins < 1 || batch < 1) return 0;
+  if (n_spins > MPNN_MAX_SPINS)  // + per episode Z/h ping-pong rows and e rows (mpnn_forward_large_kernel)
+    return 256 + (size_t)batch * ((n_spins + 15) & ~15) * 64 * 3 * sizeof(float);
   return 256;  // the call-scope norm.max() slot
 }
 
@@ -855,6 +1028,15 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     call_maxdeg_kernel<<<min(256, (batch + 255) / 256), 256, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
   if (dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_forward_dense_launch(a, saved != nullptr, st);
+  if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
+    if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
+    const int rows_pad = (N + 15) & ~15;
+    const size_t lds = ((size_t)2 * 64 * LDW + readout_scratch_floats(rows_pad, 1, 8, true)) * sizeof(float);
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_large_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    mpnn_forward_large_kernel<8><<<batch, 512, lds, st>>>(a, (float*)((char*)workspace + 256));
+    return check_launch("mpnn_forward_large");
+  }
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(N, a.gpb, false);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");
@@ -893,6 +1075,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   int rc = prepare(a, packed, n_obs_in, gs, graph_ids, batch, obs_x, ECO_NORM_PER_CALL);
   if (rc) return rc;
   if (!saved || !dq || !gradws) return fail(ECO_ERR_ARG, "null saved/dq/workspace");
+  if (a.N > MPNN_MAX_SPINS) return fail(ECO_ERR_ARG, "MPNN backward supports N <= 512");
   a.sv = (float*)saved;
   a.dq = dq;
   a.gr = (float*)gradws;

@@ -109,6 +109,8 @@ __device__ __forceinline__ int2 pack_row_info(const MpnnArgs& a, int blk, int r,
   return make_int2(b, (e - b) | (nrm << 16));
 }
 
+__device__ __forceinline__ RowInfo row_info_packed(int2 p) { return RowInfo{p.x, p.x + (p.y & 0xFFFF), p.y >> 16}; }
+
 __device__ __forceinline__ RowInfo row_info(const int2* RI, int r) {
   const int2 p = RI[r];
   return RowInfo{p.x, p.x + (p.y & 0xFFFF), p.y >> 16};
@@ -184,7 +186,7 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* hg = Hs + gl * N * ldh;
       float cs = 0.f;
-      for (int v = w; v < N; v += NW) cs += hg[v * LDH + lane];
+      for (int v = w; v < N; v += NW) cs += hg[v * ldh + lane];
       Red[(gl * NW + w) * 64 + lane] = cs;
     }
     __syncthreads();
@@ -197,7 +199,7 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
       for (int k = 0; k < NW; ++k) cs += Red[(gl * NW + k) * 64 + lane];  // fixed order
     } else {
       const float* hg = Hs + gl * N * ldh;
-      for (int v = 0; v < N; ++v) cs += hg[v * LDH + lane];
+      for (int v = 0; v < N; ++v) cs += hg[v * ldh + lane];
     }
     const float mean = cs / (float)N;
     const float* wp = P + PK_WP + lane * 64;

@@ -5,7 +5,9 @@ episodes from random initial spins (all attempts in ONE batch on the device: MPN
 forward + fused argmax + env step per vector step), and a Greedy run from each of the
 same random initialisations.  Returns the reference's DataFrame columns.
 """
+import os
 import time
+from collections import namedtuple
 
 import numpy as np
 import pandas as pd
@@ -15,6 +17,45 @@ from . import _lib
 from .envs.batched import VecSpinSystem
 from .envs.utils import SpinBasis
 from .graphs import GraphStore
+
+
+Graph = namedtuple('Graph', 'name n_vertices n_edges matrix bk_val bk_sol')
+
+
+def read_mc(path):
+    """GSet / MaxCut `.mc` instance (experiments/utils.py:400-409): first line `n m`, then `i j w` per edge,
+    1-based.  Returns (n, m, i, j, w) with 0-based endpoints."""
+    with open(path) as f:
+        head = f.readline().split()
+        if len(head) != 2:
+            raise ValueError("First line in file should define graph dimensions.")
+        n, m = int(head[0]), int(head[1])
+        rows = np.loadtxt(f, dtype=np.int64, ndmin=2)
+    if rows.size == 0:
+        rows = np.zeros((0, 3), np.int64)
+    if rows.shape[1] != 3:
+        raise ValueError("edge lines must be `i j w`")
+    return n, m, rows[:, 0] - 1, rows[:, 1] - 1, rows[:, 2]
+
+
+def load_graph(graph_dir, graph_name, dense=True):
+    """experiments/utils.py:391-418: instances/<name>.mc, bkvl/<name>.bkvl, bksol/<name>.bksol.
+    `matrix` is the reference's dense f64 adjacency (dense=False: a single-graph GraphStore instead, so
+    G22-size graphs never materialise N x N on the host).  The best-known solution gets the reference's
+    appended random 'no-action' spin (utils.py:416)."""
+    n, m, i, j, w = read_mc(os.path.join(graph_dir, 'instances', graph_name + '.mc'))
+    if dense:
+        matrix = np.zeros((n, n))
+        matrix[i, j] = w
+        matrix[j, i] = w
+    else:
+        matrix = GraphStore.from_edges(n, i, j, w)
+    with open(os.path.join(graph_dir, 'bkvl', graph_name + '.bkvl')) as f:
+        bk_val = float(f.readline())
+    with open(os.path.join(graph_dir, 'bksol', graph_name + '.bksol')) as f:
+        s = f.readline().strip()
+        bk_sol = np.array([int(ch) for ch in s] + [np.random.choice([0, 1])])
+    return Graph(graph_name, n, m, matrix, bk_val, bk_sol)
 
 
 def _greedy(env):

@@ -47,6 +47,31 @@ def dense_to_csr(matrices):
     return row_ptr, bases, edges
 
 
+def edges_to_csr(n, i, j, w):
+    """One graph from an undirected edge list (each edge once, 0-based) -> (row_ptr [1][N+1], edge_base [1],
+    edges): the CSR of the symmetric matrix load_graph builds (matrix[[i,j],[j,i]] = w), without the dense
+    N x N array (GSet graphs, N = 800 .. 20,000).  A repeated pair keeps its last weight, as the reference."""
+    i, j, w = (np.asarray(v, dtype=np.int64) for v in (i, j, w))
+    if i.size and (min(i.min(), j.min()) < 0 or max(i.max(), j.max()) >= n):
+        raise ValueError("edge endpoint out of range")
+    if np.any(i == j):
+        raise ValueError("self-loops are not allowed (zero diagonal)")
+    key = np.minimum(i, j) * n + np.maximum(i, j)
+    _, last = np.unique(key[::-1], return_index=True)   # last occurrence of every pair
+    keep = np.sort(key.size - 1 - last)
+    i, j, w = i[keep], j[keep], w[keep]
+    nz = w != 0
+    i, j, w = i[nz], j[nz], w[nz]
+    r = np.concatenate([i, j])
+    c = np.concatenate([j, i])
+    ww = np.concatenate([w, w])
+    order = np.lexsort((c, r))
+    r, c, ww = r[order], c[order], ww[order]
+    row_ptr = np.zeros((1, n + 1), dtype=np.int32)
+    row_ptr[0, 1:] = np.cumsum(np.bincount(r, minlength=n))
+    return row_ptr, np.zeros(1, dtype=np.int64), _pack_edges(c, ww)
+
+
 def random_csr(kind, n_graphs, n, param, seed, weights="discrete", chunk=512):
     """Seeded synthetic graph pool built directly as CSR (no dense N x N per graph).
     kind 'ER': G(n, p=param); 'BA': preferential attachment with m=param.
@@ -174,6 +199,11 @@ class GraphStore:
     @classmethod
     def from_dense(cls, matrices, device="cuda"):
         return cls(*dense_to_csr(matrices), device=device)
+
+    @classmethod
+    def from_edges(cls, n, i, j, w, device="cuda"):
+        """Single-graph store from an undirected edge list (GSet .mc instances, load_gset)."""
+        return cls(*edges_to_csr(n, i, j, w), device=device)
 
     @classmethod
     def random(cls, kind, n_graphs, n, param, seed=0, weights="discrete", device="cuda"):

@@ -1,0 +1,58 @@
+"""GSet `.mc` loading (experiments/utils.py:391-418) and the edge-list CSR builder (CPU only).
+The reference ships no .mc instance (gset pickles are in .MISSING_LARGE_BLOBS), so a small instance
+in the documented format is written here."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "eco-dqn_amd"))
+
+
+def _write_instance(root, name, n, edges, bk_val, bk_sol):
+    for sub in ("instances", "bkvl", "bksol"):
+        os.makedirs(os.path.join(root, sub), exist_ok=True)
+    with open(os.path.join(root, "instances", name + ".mc"), "w") as f:
+        f.write(f"{n} {len(edges)}\n")
+        for i, j, w in edges:
+            f.write(f"{i} {j} {w}\n")
+    with open(os.path.join(root, "bkvl", name + ".bkvl"), "w") as f:
+        f.write(f"{bk_val}\n")
+    with open(os.path.join(root, "bksol", name + ".bksol"), "w") as f:
+        f.write(bk_sol + "\n")
+
+
+def test_load_graph_matches_reference_semantics(tmp_path):
+    from eco_hip.experiments import load_graph, read_mc
+    edges = [(1, 2, 1), (2, 3, 1), (1, 4, -1), (3, 4, 1), (4, 5, 1)]
+    _write_instance(str(tmp_path), "G0", 5, edges, 4, "10101")
+    g = load_graph(str(tmp_path), "G0")
+    ref = np.zeros((5, 5))
+    for i, j, w in edges:  # matrix[[i,j],[j,i]] = w with 1-based ids (utils.py:408-409)
+        ref[[i - 1, j - 1], [j - 1, i - 1]] = w
+    np.testing.assert_array_equal(g.matrix, ref)
+    assert (g.name, g.n_vertices, g.n_edges, g.bk_val) == ("G0", 5, 5, 4.0)
+    assert list(g.bk_sol[:5]) == [1, 0, 1, 0, 1] and len(g.bk_sol) == 6
+    n, m, i, j, w = read_mc(os.path.join(str(tmp_path), "instances", "G0.mc"))
+    assert (n, m) == (5, 5) and list(i) == [0, 1, 0, 2, 3]
+
+
+def test_edges_to_csr_equals_dense_to_csr():
+    from eco_hip.graphs import edges_to_csr, dense_to_csr
+    rng = np.random.default_rng(0)
+    n = 300
+    iu, ju = np.triu_indices(n, 1)
+    keep = rng.random(iu.size) < 0.02
+    i, j = iu[keep], ju[keep]
+    w = rng.choice([-1, 1], i.size)
+    # shuffled endpoints and a duplicated pair (the last weight wins, as matrix[[i,j],[j,i]] = w)
+    flip = rng.random(i.size) < 0.5
+    a, b = np.where(flip, j, i), np.where(flip, i, j)
+    a = np.append(a, a[0]); b = np.append(b, b[0]); w = np.append(w, -w[0])
+    m = np.zeros((n, n))
+    for x, y, v in zip(a, b, w):
+        m[x, y] = m[y, x] = v
+    rp1, _, e1 = edges_to_csr(n, a, b, w)
+    rp2, _, e2 = dense_to_csr([m])
+    np.testing.assert_array_equal(rp1, rp2)
+    np.testing.assert_array_equal(e1, e2)

@@ -1,0 +1,94 @@
+"""N > 512 (GSet G22-size graphs): the global-memory MPNN forward
+(mpnn_forward_large_kernel) against the fp32 torch oracle, the batched env at N = 2000 against the CPU
+oracle, and the boundary errors of the inference-only large path.
+
+Bars: Q within 5e-5 (1 + |q|) of the oracle (f32, other summation order); env rewards / spins bit-exact.
+G22 itself is absent from the reference (.MISSING_LARGE_BLOBS:1): a seeded ER(N, p) graph with unit
+weights stands in (G22 is an unweighted 2000-vertex, 19,990-edge random graph)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import graphs as og
+from oracle import mpnn_oracle as mo
+from oracle import spinsystem_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+
+def _scaled_err(a, b):
+    return float(((a - b).abs() / (1 + b.abs())).max())
+
+
+@pytest.mark.parametrize("n,B,p", [(600, 3, 0.02), (1000, 2, 0.01)])
+def test_large_forward_matches_oracle(n, B, p):
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ActConfig, ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL
+    rng = np.random.default_rng(n)
+    mats = [og.er_graph(n, p, rng, weights="uniform" if b % 2 else "discrete") for b in range(B)]
+    store = GraphStore.from_dense(mats)
+    g = torch.Generator().manual_seed(n)
+    w = mo.init_weights(g, std=0.1)
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    gids = torch.arange(B, dtype=torch.int32, device="cuda")
+    q = net.forward_graphs(x.cuda(), store, gids, norm_scope=ECO_NORM_PER_GRAPH).cpu()
+    for b in range(B):
+        obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), mats[b]])).float()
+        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-5
+    # per-call norm scope + fused greedy act = argmax of the returned Q
+    acts = torch.empty(B, dtype=torch.int32, device="cuda")
+    qc = torch.empty(B, n, device="cuda")
+    net.forward_graphs(x.cuda(), store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=qc,
+                       act=ActConfig(0.0, 1, 0.0, 1, 0), actions_out=acts)
+    assert torch.equal(acts.long(), qc.argmax(1))
+
+
+def test_large_training_forward_and_backward_are_rejected():
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    n = 600
+    store = GraphStore.from_dense([og.er_graph(n, 0.01, np.random.default_rng(0))])
+    net = MPNN(device="cuda")
+    x = torch.zeros(1, n, 8, device="cuda")
+    gids = torch.zeros(1, dtype=torch.int32, device="cuda")
+    saved = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        net.forward_graphs(x, store, gids, norm_scope=1, saved=saved)
+
+
+def test_env_n2000_matches_oracle():
+    """20 random flips of 4 episodes on one G22-like graph: rewards, dones and spins bit-exact."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    n, B, T = 2000, 4, 4000
+    rng = np.random.default_rng(22)
+    J = og.er_graph(n, 0.01, rng, weights="uniform")
+    store = GraphStore.from_dense([J])
+    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
+    spins = 2 * rng.integers(0, 2, (B, n)) - 1
+    env.reset(graph_ids=np.zeros(B, dtype=np.int64), spins=spins)
+    oracles = []
+    for b in range(B):
+        o = so.SpinSystemOracle(J, T, basin_reward=1. / n)
+        o.reset(spins=spins[b])
+        oracles.append(o)
+    act = torch.zeros(B, dtype=torch.int32, device="cuda")
+    for t in range(20):
+        a = rng.integers(0, n, B)
+        act.copy_(torch.from_numpy(a).to(torch.int32))
+        _, r, d = env.step(act)
+        r = r.cpu().numpy()
+        for b, o in enumerate(oracles):
+            _, orew, odone, _ = o.step(int(a[b]))
+            assert r[b] == orew and bool(d[b]) == odone
+    st = env.read(spins=True)
+    for b, o in enumerate(oracles):
+        np.testing.assert_array_equal(st["spins"][b].cpu().numpy(), o.state[0].astype(np.int8))
