@@ -92,7 +92,11 @@ def main():
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--minibatch", type=int, default=2048, help="M graphs per gradient step")
-    ap.add_argument("--workload", default="train", choices=["train", "rollout"])
+    ap.add_argument("--workload", default="train", choices=["train", "rollout", "gset", "er20"],
+                    help="train = configs[2] (default); rollout = its act + env step half; "
+                         "gset = configs[4] per GPU: 1024 episodes of greedy best-cut search on one "
+                         "G22-like ER(2000, p=0.01) unit-weight graph; er20 = configs[1]: 4096 ER-20 "
+                         "episodes, MPNN forward + greedy act + env step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -105,6 +109,9 @@ def main():
         torch.distributed.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    if args.workload in ("gset", "er20"):
+        return inference_bench(args, world, rank, dev, dist)
 
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
@@ -205,6 +212,91 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(n, train=train)
+        print(json.dumps(out))
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+def inference_bench(args, world, rank, dev, dist):
+    """configs[4] (gset) / configs[1] (er20): batched greedy rollouts, one vector step = MPNN forward +
+    fused greedy argmax (dqn.py:490-512 via experiments/utils.py:154-187) + env step for every episode."""
+    from eco_hip import _lib
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.parallel import max_over_ranks, best_cut_over_ranks
+    seed = 1234 + rank
+    if args.workload == "gset":
+        # G22 is absent from the reference (.MISSING_LARGE_BLOBS:1): unweighted ER(2000, 0.01) stand-in
+        n, B, kind, p, weights, ngraphs = 2000, 1024, "ER", 0.01, "uniform", 1
+        T = 2 * n  # step_factor 2 (experiments/test_eco.py:84)
+    else:
+        n, B, kind, p, weights, ngraphs = 20, 4096, "ER", 0.15, "discrete", 4096
+        T = 2 * n
+    store = GraphStore.random(kind, ngraphs, n, p, seed=1234, weights=weights, device=dev)
+    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
+    net = MPNN(device=dev)
+    net.init_normal_(0.1, generator=torch.Generator().manual_seed(0))
+    gids_np = np.arange(B) % ngraphs
+    env.reset(graph_ids=gids_np, seed=seed)
+    gids = env.graph_ids
+    acts = torch.empty(B, dtype=torch.int32, device=dev)
+    greedy = _lib.ActConfig(0.0, 1, 0.0, 0, 0)
+    timers = []
+    net.timer = timers
+
+    def one_step():
+        net.forward_graphs(env.obs_x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, act=greedy, actions_out=acts)
+        env.step(acts)
+
+    for _ in range(max(args.warmup, 1)):
+        one_step()
+    torch.cuda.synchronize()
+    timers.clear()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0, device=dev)
+    net.timer = None
+    fwd_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timers) / max(len(timers), 1)
+    nnz = int(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
+    fl = mpnn_flops(nnz, n) * B
+    st = env.read(best_spins=True)
+    best = st["best_solution"].double()
+    i = int(best.argmax())
+    best_cut, _ = best_cut_over_ranks(float(best[i]), st["best_spins"][i], device=dev)
+    if rank == 0:
+        name = "GSet G22-like (ER 2000, p=0.01, unit weights)" if args.workload == "gset" else "ER_20spin"
+        out = {
+            "metric": "env-steps/sec (batched episodes) on " + name + " MaxCut",
+            "value": B * args.steps * world / dt,
+            "unit": "env-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (MPNN on f32-exact MFMA / bf16x3 splits) / f64+int (env)",
+            "data": "synthetic: seeded graphs; random-init MPNN (std 0.1)",
+            "config": {"workload": f"{name} x{B} episodes/GPU: MPNN fwd + greedy act + env step "
+                                   f"({'configs[4]' if args.workload == 'gset' else 'configs[1]'})",
+                       "n_spins": n, "envs_per_gpu": B, "graphs": ngraphs, "max_steps": T,
+                       "parallelism": f"episodes sharded, dp{world}, no collective until the best-cut reduce"},
+            "roofline": {"bound": "mfma", "kernel": "mpnn_forward", "achieved": fl / (fwd_ms * 1e-3) / 1e12,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": fl / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "avg_launch_ms": fwd_ms, "flops_per_launch": fl},
+            "best_cut_after_steps": best_cut,
+        }
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()
