@@ -107,10 +107,10 @@ __device__ __forceinline__ void dense_agg(f32x4 (&acc)[4], const uint16_t* PL, c
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;  // piece position: (j >> 2) & 3 == q for every row read here
-#pragma unroll
-  for (int kc = 0; kc < DN_KC; ++kc) {
-    if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
-    const bf16x8 bf = adj_frag<MODE>((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+#pragma unroll 1
+  for (int kc = kc0; kc < kc1; ++kc) {  // not unrolled: bounds the fragment reads in flight (16-wave VGPR budget)
+    const uint32_t wd = kc < 2 ? adjb[0] : kc < 4 ? adjb[1] : kc < 6 ? adjb[2] : adjb[3];
+    const bf16x8 bf = adj_frag<MODE>((wd >> (16 * (kc & 1))) & 0xFFFFu);
     const uint16_t* base = PL + (32 * kc + j_in) * 16 + 4 * pc;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {

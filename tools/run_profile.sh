@@ -2,7 +2,7 @@
 # rocprofv3 passes for the bench workload (run on the GPU box via gpurun):
 #   1) kernel trace + stats  2) FETCH_SIZE  3) WRITE_SIZE   (separate PMC passes,
 #   MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of wide streaming reads on gfx950)
-# usage: bash profiles/run_profile.sh <tag> [bench args...]
+# usage: bash tools/run_profile.sh <tag> [bench args...]
 set -euo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
