@@ -84,6 +84,32 @@ def cpu_baseline(n=200, seconds=12.0, train=True):
                        f"(numpy SpinSystem restatement + torch-CPU MPNN, B=1)")
 
 
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v2", "pmc_hbm.json")
+
+
+def pmc_traffic(dom, B, M, n):
+    """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC pass of this
+    workload (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction), averaged over the
+    launch mix the live timing averages over; None when no matching measurement is committed."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            k = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    gpb = 1 if n >= 208 else 208 // n
+    try:
+        if dom == "mpnn_forward_kernel":
+            fw = k["mpnn_forward_dense_kernel"]
+            act, tr = fw[str((B + gpb - 1) // gpb)], fw[str((M + gpb - 1) // gpb)]
+            return (act["hbm_bytes_per_launch"] + 3 * (B * 2 // M) * tr["hbm_bytes_per_launch"]) / \
+                (1 + 3 * (B * 2 // M))
+        bw = k["mpnn_backward_dense_kernel"][str((M + gpb - 1) // gpb)]
+        wg = next(iter(k["wgrad_kernel"].values()))
+        return bw["hbm_bytes_per_launch"] + wg["hbm_bytes_per_launch"]
+    except (KeyError, StopIteration):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,7 +231,9 @@ def main():
                        "train_minibatch": args.minibatch, "grad_steps_per_vector_step": agent._k_per_vec if train else 0,
                        "replay_ratio": 2.0, "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                         "traffic": pmc_traffic(dom, B, args.minibatch, n) if train else None,
+                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v2/pmc_hbm.json)",
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
