@@ -88,7 +88,13 @@ __host__ __device__ inline FlatOffsets flat_offsets(int nobs) {
 
 // ---- saved activations of the training forward: [tensor][R][64] then per graph ----
 enum { SV_H0 = 0, SV_H1, SV_H2, SV_H3, SV_E, SV_EAGG, SV_M0, SV_M1, SV_M2, SV_AGG0, SV_AGG1, SV_AGG2,
-       SV_NODE_TENSORS };  // then MEAN [B][64], P [B][64]
+       SV_NODE_TENSORS };  // then MEAN [B][64], P [B][64], then the ReLU masks (dense path)
+// ReLU sign masks of the dense forward, read by the dense backward instead of the f32 rows:
+// uint16 [R][4 lane quarters][8 tensors], bit 4c + i = feature 16c + 4q + i > 0
+enum { SM_H0 = 0, SM_H1, SM_H2, SM_H3, SM_E, SM_M0, SM_M1, SM_M2, SM_TENSORS };
+__host__ __device__ inline size_t sv_mask_offset_floats(size_t RT, size_t B) {
+  return (size_t)SV_NODE_TENSORS * RT * 64 + 2 * B * 64;
+}
 
 // ---- backward gradient workspace: [tensor][R][64] then per graph / per block ----
 enum { GR_DUU0 = 0, GR_DUU1, GR_DUU2, GR_DUM0, GR_DUM1, GR_DUM2, GR_DUE, GR_DU0, GR_DZ, GR_DE, GR_DH,

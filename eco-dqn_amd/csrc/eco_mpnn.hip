@@ -955,7 +955,8 @@ extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
 
 extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
   if (n_spins < 1 || batch < 1) return 0;
-  return ((size_t)SV_NODE_TENSORS * n_spins * batch * 64 + 2 * (size_t)batch * 64) * sizeof(float);
+  const size_t RT = (size_t)n_spins * batch;
+  return sv_mask_offset_floats(RT, batch) * sizeof(float) + RT * 4 * SM_TENSORS * sizeof(uint16_t);
 }
 
 struct KCfg {

@@ -219,6 +219,18 @@ __device__ __forceinline__ float4 masked(const f32x4& v, uint32_t m, int c) {
                      (m >> (4 * c + 2)) & 1u ? v[2] : 0.f, (m >> (4 * c + 3)) & 1u ? v[3] : 0.f);
 }
 
+// store the lane's 16-bit ReLU mask of tensor t for block row r (saved-activation mask region)
+__device__ __forceinline__ void store_mask(const MpnnArgs& a, size_t RT, size_t grow, int q, int t, uint32_t m) {
+  uint16_t* M = reinterpret_cast<uint16_t*>(a.sv + sv_mask_offset_floats(RT, a.B));
+  M[(grow * 4 + q) * SM_TENSORS + t] = (uint16_t)m;
+}
+
+// 16-bit mask of tensor t from a lane's 8 packed masks
+__device__ __forceinline__ uint32_t mask16(const uint4& m, int t) {
+  const uint32_t wd = t < 2 ? m.x : t < 4 ? m.y : t < 6 ? m.z : m.w;
+  return (wd >> (16 * (t & 1))) & 0xFFFFu;
+}
+
 // LDS-DMA copy of n_frag 1-KB weight fragments (global -> LDS, both contiguous, no registers):
 // wave w issues fragments w, w + NW, ...  Retire with glds_wait() before the barrier that publishes them.
 template <int NW>
@@ -265,20 +277,14 @@ int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st)
   return check_launch("graphs_adjbits");
 }
 
-// The lane's adjacency operand (adj_bits16 of every k-chunk, packed in 4 words): read from the prepared
-// gs.adjbits when the block holds one graph, else built here from the CSR rows in ADJ (LDS scratch of
-// rows_pad * DN_ADJW words, free again on return).  RI and GB must be staged (and a barrier passed).
+// Block bitmask adjacency, built in ADJ (LDS scratch of rows_pad * DN_ADJW words) from the CSR rows;
+// unnecessary (returns false) when the block holds one graph with a prepared gs.adjbits.  RI and GB must
+// be staged (and a barrier passed).  Uniform over the workgroup (contains barriers).
 template <int NT>
-__device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ, const int2* RI, const int64_t* GB,
-                                                int blk, int rows_pad, int rows_valid, int r, int rr, bool valid,
-                                                int s4, uint32_t (&adjb)[4]) {
+__device__ __forceinline__ bool adj_build(const MpnnArgs& a, uint32_t* ADJ, const int2* RI, const int64_t* GB,
+                                          int rows_pad, int rows_valid) {
   const int N = a.N;
-  if (a.gpb == 1 && a.gs.adjbits != nullptr) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)a.gids[blk] * N + r) * 4 + s4) * 4);
-    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
-    return;
-  }
+  if (a.gpb == 1 && a.gs.adjbits != nullptr) return false;
   for (int i = threadIdx.x; i < rows_pad * DN_ADJW; i += NT) ADJ[i] = 0u;
   __syncthreads();
   // 4 threads per row, 8 edge loads in flight per thread
@@ -305,6 +311,18 @@ __device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ
     }
   }
   __syncthreads();
+  return true;
+}
+
+// The lane's adjacency operand (adj_bits16 of every k-chunk, packed in 4 words) for block row r.
+__device__ __forceinline__ void adj_lane(const MpnnArgs& a, const uint32_t* ADJ, bool built, int blk, int r, int rr,
+                                         bool valid, int s4, uint32_t (&adjb)[4]) {
+  if (!built) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)a.gids[blk] * a.N + r) * 4 + s4) * 4);
+    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
+    return;
+  }
   const uint2* arow = reinterpret_cast<const uint2*>(ADJ + rr * DN_ADJW);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -312,7 +330,16 @@ __device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ
     const uint32_t hi = 2 * k + 1 < DN_KC ? adj_bits16(arow[2 * k + 1], s4) : 0u;
     adjb[k] = lo | (hi << 16);
   }
-  __syncthreads();
+}
+
+// The lane's adjacency operand: prepared gs.adjbits, or built here (ADJ free again on return).
+template <int NT>
+__device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ, const int2* RI, const int64_t* GB,
+                                                int blk, int rows_pad, int rows_valid, int r, int rr, bool valid,
+                                                int s4, uint32_t (&adjb)[4]) {
+  const bool built = adj_build<NT>(a, ADJ, RI, GB, rows_pad, rows_valid);
+  adj_lane(a, ADJ, built, blk, r, rr, valid, s4, adjb);
+  if (built) __syncthreads();
 }
 
 // LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
@@ -448,6 +475,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
       ereg[nt] = relu4(d[nt]);
       if (SAVE && valid) st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, ereg[nt]);
     }
+    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_E, pos_mask(ereg));
   }
   __syncthreads();  // every wave is done with the V planes and with Wf
   ECO_TS(3);
@@ -481,6 +509,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
                           lo(u1.y) + lo(u2.y) + lo(u3.y), hi(u1.y) + hi(u2.y) + hi(u3.y));
     if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
   }
+  if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H0, pos_mask(hreg));
   ECO_TS(4);
 
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
@@ -520,6 +549,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
       float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
       for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
+      store_mask(a, RT, R0 + r, s4, SM_M0 + layer, pos_mask(mrel));
     }
     __syncthreads();  // B2: all waves done with Wm and with the planes of h_layer
     glds_frags<NW>(WP, Wub + BF_HALF, 24, w, lane);
@@ -536,6 +566,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
       hreg[c] = valid ? relu4(hn[c]) : zero4();
       if (SAVE && valid) st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
     }
+    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H1 + layer, pos_mask(hreg));
     if (layer < 2 && has_tile) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) plane_store4(PL, c, r, s4, hreg[c]);
@@ -562,13 +593,15 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
 // dense aggregation of the forward (A symmetric), every Linear a transposed bf16x3 product (BFT_*
 // fragments).  Writes the pre-activation gradients the weight-gradient reduction reads (GR_DUU*, GR_DUM*,
 // GR_DUE, GR_DU0, GR_DZ) and the per-graph / per-block partials of the CSR backward; dh and de stay in
-// registers (no GR_DE / GR_DH round trips).
+// registers (no GR_DE / GR_DH round trips), and the forward's ReLU decisions come from 16-bit masks it
+// saved (SM_*) instead of re-reading the f32 activation rows.  NW waves own MAXT 16-node tiles each
+// (t = w + ti NW).
 // LDS: PL planes of the gathered gradient G (readout scratch first) | WP 48 fragments | WX 24 fragments |
 //      RI [rows_pad] int2 | GB [gpb] i64
-__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense_kernel(MpnnArgs a) {
+template <int NW, int MAXT>
+__global__ __launch_bounds__(64 * NW, 1) void mpnn_backward_dense_kernel(MpnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   ECO_TS(16);
-  constexpr int NW = DN_NW;
   constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
@@ -608,17 +641,32 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense_kernel(Mpnn
   for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
   for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
   __syncthreads();
-  const bool has_tile = w < ntiles;
-  const int r = w * 16 + c16;
-  const bool valid = has_tile && r < rows_valid;
-  const int rr = min(r, rows_pad - 1);
-  const RowInfo ri = row_info(RI, rr);
-  const float nf = (float)ri.norm;
-  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
-  const int kc0 = (g_lo * N) >> 5;
-  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
-  uint32_t adjb[4];
-  dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
+  // per tile: node, validity, norm, k-chunk range, adjacency bits
+  bool has_tile[MAXT], valid[MAXT];
+  int rw[MAXT], rr[MAXT], kc0[MAXT], kc1[MAXT];
+  float nf[MAXT];
+  uint32_t adjb[MAXT][4];
+  uint4 rmask[MAXT];  // the forward's ReLU masks of this lane's node (SM_* tensors, 16 bits each)
+  {
+    const bool built = adj_build<NT>(a, ADJ, RI, GB, rows_pad, rows_valid);
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const int t = w + ti * NW;
+      has_tile[ti] = t < ntiles;
+      rw[ti] = t * 16 + c16;
+      valid[ti] = has_tile[ti] && rw[ti] < rows_valid;
+      rr[ti] = min(rw[ti], rows_pad - 1);
+      nf[ti] = (float)row_info(RI, rr[ti]).norm;
+      const int g_lo = min(t * 16, rows_pad - 1) / N, g_hi = min(t * 16 + 15, rows_pad - 1) / N;
+      kc0[ti] = (g_lo * N) >> 5;
+      kc1[ti] = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+      adj_lane(a, ADJ, built, blk, rw[ti], rr[ti], valid[ti], s4, adjb[ti]);
+      const uint16_t* M = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
+      rmask[ti] = valid[ti] ? *reinterpret_cast<const uint4*>(M + ((R0 + rw[ti]) * 4 + s4) * SM_TENSORS)
+                            : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (built) __syncthreads();
+  }
   ECO_TS(17);
 
   // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
@@ -669,16 +717,17 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense_kernel(Mpnn
   }
   __syncthreads();
   // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
-  float4 dh[4];
-  {
-    const float dqi = valid ? DQ[r] : 0.f;
-    const int gl = rr / N;
+  float4 dh[MAXT][4];
+#pragma unroll
+  for (int ti = 0; ti < MAXT; ++ti) {
+    const float dqi = valid[ti] ? DQ[rw[ti]] : 0.f;
+    const int gl = rr[ti] / N;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int f = 16 * c + 4 * s4;
-      const float4 dm = valid ? f4(DMEAN + gl * 64 + f) : zero4();
-      dh[c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
-                          fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
+      const float4 dm = valid[ti] ? f4(DMEAN + gl * 64 + f) : zero4();
+      dh[ti][c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
+                              fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
     }
   }
   __syncthreads();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes (0 * garbage = NaN)
@@ -695,157 +744,181 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense_kernel(Mpnn
   // ---- update layers in reverse (mpnn.py:114-120) ----
   // [B0: Wu^T in WP, Wm^T(dagg half) in WX; planes free] dh_direct, dm | [B1] DMA Wm^T(de half) -> WP;
   // dagg -> G planes | [B2] de; DMA next Wm^T(dagg half) -> WX; dh = dh_direct + A.G | [B3] DMA next Wu^T -> WP
-  float4 de[4];
+  float4 de[MAXT][4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) de[c] = zero4();
+  for (int ti = 0; ti < MAXT; ++ti)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) de[ti][c] = zero4();
   for (int layer = 2; layer >= 0; --layer) {
     const uint16_t* WmT = PB + BFT_LAYER + layer * BF_LAYER_STRIDE;
-    const size_t ro = (R0 + rr) * 64 + 4 * s4;
-    // duu = dh' * [h' > 0]
-    float4 duu[4];
-    uint32_t mmask;
-    {
-      float4 hv[4], mv[4];
+    // duu = dh' * [h' > 0]  (in place in dh), m > 0 masks
+    uint32_t mmask[MAXT];
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
+      mmask[ti] = mask16(rmask[ti], SM_M0 + layer);
+      const uint32_t hmask = mask16(rmask[ti], SM_H0 + layer + 1);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        hv[c] = valid ? f4(SV(SV_H0 + layer + 1) + ro + 16 * c) : zero4();
-        mv[c] = valid ? f4(SV(SV_M0 + layer) + ro + 16 * c) : zero4();
-      }
-      mmask = pos_mask(mv);
-      const uint32_t hmask = pos_mask(hv);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        duu[c] = masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, hmask, c);
-        if (valid) st4(GR(GR_DUU0 + layer) + ro + 16 * c, duu[c]);
+        dh[ti][c] = masked(f32x4{dh[ti][c].x, dh[ti][c].y, dh[ti][c].z, dh[ti][c].w}, hmask, c);
+        if (valid[ti]) st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[ti][c]);
       }
     }
+    if (layer == 1) ECO_TS(24);
     glds_wait();
     __syncthreads();  // B0
-    // [dh_direct, dm] = Wu^T . duu
-    f32x4 dhd[4], dmm[4];
+    if (layer == 1) ECO_TS(25);
+    // [dh_direct, dm] = Wu^T . duu;  dum = dm * [m > 0]
+    f32x4 dhd[MAXT][4];
+    float4 dum[MAXT][4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      dhd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dmm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (has_tile) mm_bf3x2(dhd, dmm, duu, WP, WP + BF_HALF, lane);
-    // dum = dm * [m > 0]
-    float4 dum[4];
+    for (int ti = 0; ti < MAXT; ++ti) {
+      f32x4 dmm[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      dum[c] = masked(dmm[c], mmask, c);
-      if (valid) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
+      for (int nt = 0; nt < 4; ++nt) {
+        dhd[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dmm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (has_tile[ti]) mm_bf3x2(dhd[ti], dmm, dh[ti], WP, WP + BF_HALF, lane);
+      const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dum[ti][c] = masked(dmm[c], mmask[ti], c);
+        if (valid[ti]) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[ti][c]);
+      }
     }
+    if (layer == 1) ECO_TS(26);
     __syncthreads();  // B1: WP free
+    if (layer == 1) ECO_TS(27);
     glds_frags<NW>(WP, WmT + BF_HALF, 24, w, lane);  // Wm^T, de half
     // dagg = Wm^T(agg half) . dum;  G = dagg / norm (d agg / d(A.h) = 1/norm) -> planes
-    f32x4 dg[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) {
-      mm_bf3(dg, dum, WX, lane);
+    for (int ti = 0; ti < MAXT; ++ti) {
+      if (!has_tile[ti]) continue;  // wave-uniform
+      f32x4 dg[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mm_bf3(dg, dum[ti], WX, lane);
+      const float n_ = nf[ti];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        plane_store4(PL, c, r, s4, valid ? make_float4(dg[c][0] / nf, dg[c][1] / nf, dg[c][2] / nf, dg[c][3] / nf)
-                                         : zero4());
+        plane_store4(PL, c, rw[ti], s4,
+                     valid[ti] ? make_float4(dg[c][0] / n_, dg[c][1] / n_, dg[c][2] / n_, dg[c][3] / n_) : zero4());
     }
+    if (layer == 1) ECO_TS(28);
     glds_wait();
     __syncthreads();  // B2: G planes complete, Wm^T de half landed, WX free
+    if (layer == 1) ECO_TS(29);
     if (layer > 0) glds_frags<NW>(WX, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE, 24, w, lane);
     else glds_frags<NW>(WX, PB + BFT_WF, 24, w, lane);  // Wf^T for the edge layer
-    f32x4 dd[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) dd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) mm_bf3(dd, dum, WP, lane);
+    for (int ti = 0; ti < MAXT; ++ti) {
+      f32x4 dd[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      de[c].x += dd[c][0]; de[c].y += dd[c][1]; de[c].z += dd[c][2]; de[c].w += dd[c][3];
+      for (int nt = 0; nt < 4; ++nt) dd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (has_tile[ti]) mm_bf3(dd, dum[ti], WP, lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        de[ti][c].x += dd[c][0]; de[ti][c].y += dd[c][1]; de[ti][c].z += dd[c][2]; de[ti][c].w += dd[c][3];
+      }
+      // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
+      if (has_tile[ti]) dense_agg<0>(dhd[ti], PL, adjb[ti], kc0[ti], kc1[ti], lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dh[ti][c] = valid[ti] ? as_f4(dhd[ti][c]) : zero4();
     }
-    // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
-    f32x4 ag[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) ag[nt] = dhd[nt];
-    if (has_tile) dense_agg<0>(ag, PL, adjb, kc0, kc1, lane);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) dh[c] = valid ? as_f4(ag[c]) : zero4();
+    if (layer == 1) ECO_TS(30);
     __syncthreads();  // B3: WP and the planes free
     if (layer > 0) glds_frags<NW>(WP, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE + 2 * BF_HALF, 48, w, lane);
     ECO_TS(21 - layer);
   }
 
-  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due ----
-  const size_t ro = (R0 + rr) * 64 + 4 * s4;
-  float4 due[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const float4 hv = valid ? f4(SV(SV_H0) + ro + 16 * c) : zero4();
-    const float4 ev = valid ? f4(SV(SV_E) + ro + 16 * c) : zero4();
-    if (valid) {
-      st4(GR(GR_DU0) + ro + 16 * c, make_float4(hv.x > 0.f ? dh[c].x : 0.f, hv.y > 0.f ? dh[c].y : 0.f,
-                                                hv.z > 0.f ? dh[c].z : 0.f, hv.w > 0.f ? dh[c].w : 0.f));
-    }
-    due[c] = make_float4(ev.x > 0.f ? de[c].x : 0.f, ev.y > 0.f ? de[c].y : 0.f, ev.z > 0.f ? de[c].z : 0.f,
-                         ev.w > 0.f ? de[c].w : 0.f);
-    if (valid) st4(GR(GR_DUE) + ro + 16 * c, due[c]);
-  }
+  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
   glds_wait();
   __syncthreads();  // Wf^T landed
-  {
-    f32x4 dg[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) {
+  for (int ti = 0; ti < MAXT; ++ti) {
+    const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
+    float4 due[4];
+    const uint32_t h0m = mask16(rmask[ti], SM_H0), em = mask16(rmask[ti], SM_E);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (valid[ti])
+        st4(GR(GR_DU0) + ro + 16 * c, masked(f32x4{dh[ti][c].x, dh[ti][c].y, dh[ti][c].z, dh[ti][c].w}, h0m, c));
+      due[c] = masked(f32x4{de[ti][c].x, de[ti][c].y, de[ti][c].z, de[ti][c].w}, em, c);
+      if (valid[ti]) st4(GR(GR_DUE) + ro + 16 * c, due[c]);
+    }
+    if (has_tile[ti]) {
+      f32x4 dg[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       mm_bf3(dg, due, WX, lane);
+      const float n_ = nf[ti];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        plane_store4(PL, c, r, s4, valid ? make_float4(dg[c][0] / nf, dg[c][1] / nf, dg[c][2] / nf, dg[c][3] / nf)
-                                         : zero4());
+        plane_store4(PL, c, rw[ti], s4,
+                     valid[ti] ? make_float4(dg[c][0] / n_, dg[c][1] / n_, dg[c][2] / n_, dg[c][3] / n_) : zero4());
     }
   }
   __syncthreads();
   ECO_TS(22);
   // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
   {
-    f32x4 gp[4], gm[4];
+    float dwacc[16];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      gp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 16; ++i) dwacc[i] = 0.f;
+#pragma unroll
+    for (int ti = 0; ti < MAXT; ++ti) {
+      f32x4 gp[4], gm[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        gp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (has_tile[ti]) {
+        dense_agg<1>(gp, PL, adjb[ti], kc0[ti], kc1[ti], lane);
+        dense_agg<2>(gm, PL, adjb[ti], kc0[ti], kc1[ti], lane);
+      }
+      float4 x0 = zero4(), x1 = zero4();
+      if (valid[ti]) {
+        x0 = f4(a.x + (R0 + rw[ti]) * 8);
+        x1 = f4(a.x + (R0 + rw[ti]) * 8 + 4);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float dz4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int f = 16 * c + 4 * s4 + i;
+          const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
+          const float z = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
+                          w1.z * x1.z + w1.w * x1.w;
+          const float wa = P[PK_WA + f];
+          const float tp = fmaf(1.f, wa, z) > 0.f ? gp[c][i] : 0.f;
+          const float tm = fmaf(-1.f, wa, z) > 0.f ? gm[c][i] : 0.f;
+          dz4[i] = valid[ti] ? tp + tm : 0.f;
+          dwacc[4 * c + i] += valid[ti] ? tp - tm : 0.f;
+        }
+        if (valid[ti])
+          st4(GR(GR_DZ) + (R0 + rw[ti]) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
+      }
     }
-    if (has_tile) {
-      dense_agg<1>(gp, PL, adjb, kc0, kc1, lane);
-      dense_agg<2>(gm, PL, adjb, kc0, kc1, lane);
-    }
-    float4 x0 = zero4(), x1 = zero4();
-    if (valid) {
-      x0 = f4(a.x + (R0 + r) * 8);
-      x1 = f4(a.x + (R0 + r) * 8 + 4);
+    // reduce dw_a over the 16 node lanes sharing s4, then over waves (fixed order)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float v = dwacc[i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      dwacc[i] = v;
     }
     __syncthreads();  // every wave is done reading the G planes: the region becomes the dwa scratch
     float* REDW = lds;  // [NW][64]
+    if (c16 == 0) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float dz4[4], dwa4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int f = 16 * c + 4 * s4 + i;
-        const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
-        const float z = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
-                        w1.z * x1.z + w1.w * x1.w;
-        const float wa = P[PK_WA + f];
-        const float tp = fmaf(1.f, wa, z) > 0.f ? gp[c][i] : 0.f;
-        const float tm = fmaf(-1.f, wa, z) > 0.f ? gm[c][i] : 0.f;
-        dz4[i] = valid ? tp + tm : 0.f;
-        // reduce dw_a over the 16 node lanes sharing s4
-        float v = valid ? tp - tm : 0.f;
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        dwa4[i] = v;
-      }
-      if (valid) st4(GR(GR_DZ) + (R0 + r) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
-      if (c16 == 0) st4(REDW + w * 64 + 16 * c + 4 * s4, make_float4(dwa4[0], dwa4[1], dwa4[2], dwa4[3]));
+      for (int c = 0; c < 4; ++c)
+        st4(REDW + w * 64 + 16 * c + 4 * s4,
+            make_float4(dwacc[4 * c], dwacc[4 * c + 1], dwacc[4 * c + 2], dwacc[4 * c + 3]));
     }
     __syncthreads();
     if (w == 0) {
@@ -863,9 +936,18 @@ static int mpnn_backward_dense_launch(const MpnnArgs& a, hipStream_t st) {
   const size_t lds = dense_fwd_lds_bytes(rows_pad, a.gpb);
   if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  mpnn_backward_dense_kernel<<<blocks, 64 * DN_NW, lds, st>>>(a);
+  // 16 waves x 1 tile (latency hiding; 2 VGPRs spill) is faster than 8 x 2 (no spills): 0.70 vs 0.82 ms
+  // at M=2048 ER-200.  ECO_MPNN_BWD8 selects the 8 x 2 variant for A/B measurements.
+  static const bool w8 = getenv("ECO_MPNN_BWD8") != nullptr;
+  if (!w8) {
+    (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel<16, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    mpnn_backward_dense_kernel<16, 1><<<blocks, 1024, lds, st>>>(a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel<8, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    mpnn_backward_dense_kernel<8, 2><<<blocks, 512, lds, st>>>(a);
+  }
   return check_launch("mpnn_backward_dense");
 }
 

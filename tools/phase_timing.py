@@ -84,7 +84,12 @@ def main():
     grad = torch.zeros_like(net.flat)
     net.backward_graphs(x, store, gids, saved, dq, grad)
     torch.cuda.synchronize()
-    report(f"backward          B={B} N={N}", stamps(nblk), list(range(16, 24)), BWD)
+    ts = stamps(nblk)
+    report(f"backward          B={B} N={N}", ts, list(range(16, 24)), BWD)
+    if ts is not None and ts[:, 24].any():
+        report("  layer 1 detail (wave 0)", ts, [19, 24, 25, 26, 27, 28, 29, 30, 20],
+               ["h,m loads + duu", "B0 wait", "Wu^T x2 + dum", "B1 wait", "dagg + G planes", "B2 wait",
+                "de + A.G", "B3 wait"])
 
 
 if __name__ == "__main__":
