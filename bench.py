@@ -87,10 +87,12 @@ def cpu_baseline(n=200, seconds=12.0, train=True):
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v2", "pmc_hbm.json")
 
 
-def pmc_traffic(dom, B, M, n):
+def pmc_traffic(dom, B, M, n, graph="ER"):
     """HBM bytes per launch of the dominant kernel, from the committed rocprofv3 PMC pass of this
     workload (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction), averaged over the
     launch mix the live timing averages over; None when no matching measurement is committed."""
+    if (graph, n, B, M) != ("ER", 200, 8192, 2048):  # the profiled configuration only
+        return None
     try:
         with open(PMC_SUMMARY) as f:
             k = json.load(f)["kernels"]
@@ -118,6 +120,9 @@ def main():
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--minibatch", type=int, default=2048, help="M graphs per gradient step")
+    ap.add_argument("--graph", default="ER", choices=["ER", "BA"],
+                    help="training graphs: ER(n, p=--param) (configs[2]) or BA(n, m=--param) (configs[3])")
+    ap.add_argument("--param", type=float, default=None, help="ER p (default 0.15) / BA m (default 4)")
     ap.add_argument("--workload", default="train", choices=["train", "rollout", "gset", "er20"],
                     help="train = configs[2] (default); rollout = its act + env step half; "
                          "gset = configs[4] per GPU: 1024 episodes of greedy best-cut search on one "
@@ -149,7 +154,8 @@ def main():
     B, n = args.envs, args.n
     T = 2 * n
     seed = 1234 + rank
-    store = GraphStore.random("ER", B, n, 0.15, seed=seed, device=dev)
+    gparam = args.param if args.param is not None else (0.15 if args.graph == "ER" else 4)
+    store = GraphStore.random(args.graph, B, n, gparam, seed=seed, device=dev)
     nnz = np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1)
     gflops = np.array([mpnn_flops(z, n) for z in nnz])
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
@@ -210,12 +216,12 @@ def main():
     achieved = fl / max(ms, 1e-9) / 1e9  # TFLOP/s
     value = B * args.steps * world / dt
     if rank == 0:
-        wl = ("ER_200spin x%d envs/GPU: full ECO-DQN train loop per vector step (act + env step + replay add "
+        wl = (f"{args.graph}_{n}spin" + " x%d envs/GPU: full ECO-DQN train loop per vector step (act + env step + replay add "
               "+ %d grad steps of M=%d: sample, double-DQN TD, MPNN fwd/bwd, Adam)"
               % (B, agent._k_per_vec, args.minibatch)) if train else \
-             ("ER_200spin x%d envs/GPU: rollout only (MPNN fwd + eps-greedy act + env step + replay add)" % B)
+             (f"{args.graph}_{n}spin" + " x%d envs/GPU: rollout only (MPNN fwd + eps-greedy act + env step + replay add)" % B)
         out = {
-            "metric": "env-steps/sec (batched episodes) on ER-200 MaxCut",
+            "metric": f"env-steps/sec (batched episodes) on {args.graph}-{n} MaxCut",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -225,14 +231,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (MPNN fwd/bwd on exact-f32 MFMA) / f64+int (env)",
-            "data": "synthetic: seeded ER(200, p=0.15) +-1 graphs, one per episode; random-init MPNN (std 0.01)",
+            "dtype": "f32 (MPNN: exact bf16x3-split aggregations + six-product bf16x3 Linears, f32 accumulate; "
+                     "f32 MFMA on the CSR fallback) / f64+int (env)",
+            "data": f"synthetic: seeded {args.graph}({n}, {gparam}) +-1 graphs, one per episode; random-init MPNN "
+                    "(std 0.01)",
             "config": {"workload": wl, "n_spins": n, "envs_per_gpu": B, "max_steps": T,
                        "train_minibatch": args.minibatch, "grad_steps_per_vector_step": agent._k_per_vec if train else 0,
                        "replay_ratio": 2.0, "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(dom, B, args.minibatch, n) if train else None,
+                         "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
                          "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v2/pmc_hbm.json)",
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
