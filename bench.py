@@ -84,7 +84,7 @@ def cpu_baseline(n=200, seconds=12.0, train=True):
                        f"(numpy SpinSystem restatement + torch-CPU MPNN, B=1)")
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v2", "pmc_hbm.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v3", "pmc_hbm.json")
 
 
 def pmc_traffic(dom, B, M, n, graph="ER"):
@@ -241,7 +241,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v2/pmc_hbm.json)",
+                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v3/pmc_hbm.json)",
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},

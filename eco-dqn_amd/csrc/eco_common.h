@@ -74,6 +74,13 @@ struct alignas(16) EpScal {
   int32_t done;
   int32_t early;         // early_stopping counter
   int32_t visit_count;   // states inserted in the visited set
+  // generic scorer targets (score_solver.py:232-858); unused by the CUT kernels
+  double inorm;          // scorer._invalidity_normalizer (0 = never set: a fresh scorer's 1)
+  double lb;             // scorer._lower_bound
+  int32_t n1;            // set size #(s == +1)
+  int32_t inv;           // invalidity degree of the current spins (integer for integer weights)
+  int32_t best_n1;       // set size of best_spins
+  int32_t best_inv;      // invalidity degree of best_spins
 };
 
 // Layout of the opaque env state buffer.

@@ -12,6 +12,7 @@
 // reference, so rewards/observations match it bit for bit.
 #include "eco_common.h"
 #include "eco_mpnn.h"
+#include "eco_env_dev.h"
 
 namespace eco {
 
@@ -62,27 +63,6 @@ __global__ __launch_bounds__(256) void graphs_prepare_kernel(eco_graph_set gs, i
 }
 
 // ------------------------------------------------------------- env kernels ----
-struct EnvArgs {
-  eco_env_config cfg;
-  eco_graph_set gs;
-  EnvLayout L;
-  uint8_t* state;
-  int B;
-  const int32_t* graph_ids;
-  const int8_t* spins_in;
-  const uint8_t* mask;
-  uint64_t seed;
-  const int32_t* actions;
-  double* rewards;
-  uint8_t* dones;
-  float* obs_x;
-  double* obs_f64;
-  int32_t* err;  // device error word (first error wins)
-};
-
-__device__ __forceinline__ EpScal* scal_ptr(const EnvArgs& a) { return (EpScal*)(a.state + a.L.off_scal); }
-__device__ __forceinline__ const double* tab_ptr(const EnvArgs& a) { return (const double*)(a.state + a.L.off_tab + 256); }
-
 // time table: tab[k] = running f64 sum of k additions of 1/T (spinsystem.py:493, :506)
 __global__ void build_time_table_kernel(uint8_t* state, size_t off_tab, int T) {
   int* hdr = (int*)(state + off_tab);
@@ -112,9 +92,8 @@ __device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int 
     case ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS: return c.nqi;
     case ECO_OBS_DISTANCE_FROM_BEST_SOLUTION: return c.dist_best;
     case ECO_OBS_DISTANCE_FROM_BEST_STATE: return c.hamming;
-    case ECO_OBS_IMMEDIATE_VALIDITY_CHANGE: return 1.0;  // MaxCut: every flip valid
-    case ECO_OBS_VALIDITY_BIT: return 1.0;
-    default: return 0.0;  // validity differences are identically 0 for MaxCut
+    case ECO_OBS_VALIDITY_BIT: return 1.0;  // MaxCut: every spin vector is valid
+    default: return 0.0;  // GLOBAL_VALIDITY_DIFFERENCE: (0 - 0) / 1 (the mask observables are rejected)
   }
 }
 
@@ -138,11 +117,7 @@ __device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, con
       }
       xf[i] = (float)val;
     }
-    if (a.obs_x) {
-      float4* dst = (float4*)(a.obs_x + ((size_t)e * N + v) * ECO_MAX_OBS);
-      dst[0] = make_float4(xf[0], xf[1], xf[2], xf[3]);
-      dst[1] = make_float4(xf[4], xf[5], xf[6], xf[7]);
-    }
+    if (a.obs_x) store_obs_row(a.obs_x, (size_t)e * N + v, nobs, xf);
   }
 }
 
@@ -233,7 +208,12 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
     sc->mlr = mlr; sc->qn = qn; sc->lbabs = lbabs;
     sc->hash = 0ull; sc->t = 0; sc->hamming = 0; sc->graph = gid; sc->done = 0; sc->early = 0;
     sc->visit_count = 0;
+    sc->inorm = 1.0; sc->lb = lb; sc->inv = 0; sc->best_inv = 0;
   }
+  int n1 = 0;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) n1 += __popcll(__ballot(s[k] > 0));
+  if (lane == 0) { (scal_ptr(a) + e)->n1 = n1; (scal_ptr(a) + e)->best_n1 = n1; }
   ObsCtx c;
   c.mlr = mlr; c.dist_best = 0.0; c.hamming = 0.0; c.nqi = (double)cnt / (double)N;
   c.term = 0.0; c.ep_time = 0.0; c.basis = a.cfg.spin_basis;
@@ -310,39 +290,8 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) c += __popcll(__ballot(s[k] < 0)); return c; }();
   // HistoryBuffer.update (utils.py:444-464): is the flipped set (== spin configuration) new?
-  bool isnew = true;
-  const bool need_hist = a.cfg.has_basin_reward || a.cfg.has_stag_punishment;
-  if (need_hist) {
-    const uint64_t hash = sc->hash ^ zobrist(act);
-    const int cap = L.cap;
-    const int W = L.words;
-    uint32_t* vidx = (uint32_t*)(a.state + L.off_vidx) + (size_t)e * cap;
-    uint64_t* vh = (uint64_t*)(a.state + L.off_vhash) + (size_t)e * cap;
-    uint64_t* vst = (uint64_t*)(a.state + L.off_vstates) + (size_t)e * (T + 1) * W;
-    int slot = (int)(hash & (uint64_t)(cap - 1));
-    for (;;) {
-      const uint32_t id = vidx[slot];
-      if (id == 0u) break;
-      if (vh[slot] == hash) {
-        bool same = true;
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) same = same && (vst[(size_t)(id - 1) * W + k] == words[k]);
-        if (same) { isnew = false; break; }
-      }
-      slot = (slot + 1) & (cap - 1);
-    }
-    if (lane == 0) {
-      sc->hash = hash;
-      if (isnew) {
-        const int n = sc->visit_count;
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) vst[(size_t)n * W + k] = words[k];
-        vh[slot] = hash;
-        vidx[slot] = (uint32_t)(n + 1);
-        sc->visit_count = n + 1;
-      }
-    }
-  }
+  const bool isnew = (a.cfg.has_basin_reward || a.cfg.has_stag_punishment) ? history_update<VPT>(a, e, lane, sc, act, words)
+                                                                            : true;
   // reward (:418-457)
   double best_score = sc->best_score, best_nscore = sc->best_nscore;
   double rew = 0.0;
@@ -455,9 +404,11 @@ __global__ void env_read_kernel(EnvArgs a, double* scalars, int8_t* spins, int8_
   const int N = a.cfg.n_spins;
   const EpScal* sc = scal_ptr(a) + e;
   if (threadIdx.x == 0 && scalars) {
-    double* o = scalars + (size_t)e * 8;
+    double* o = scalars + (size_t)e * ECO_ENV_SCALARS;
     o[0] = sc->t; o[1] = sc->score; o[2] = sc->nscore; o[3] = sc->best_score;
     o[4] = sc->best_nscore; o[5] = sc->best_solution; o[6] = sc->hamming; o[7] = sc->done;
+    o[8] = sc->mlr; o[9] = sc->qn; o[10] = sc->inorm > 0.0 ? sc->inorm : 1.0; o[11] = sc->lb;
+    o[12] = sc->n1; o[13] = sc->inv; o[14] = sc->graph; o[15] = 0.0;
   }
   const int8_t* gsp = (const int8_t*)(a.state + a.L.off_spins) + (size_t)e * N;
   const int8_t* gb = (const int8_t*)(a.state + a.L.off_best) + (size_t)e * N;
@@ -473,11 +424,21 @@ static int validate_cfg(const eco_env_config* c) {
   if (c->n_spins < 1 || c->n_spins > ECO_MAX_SPINS)
     return fail(ECO_ERR_ARG, "n_spins out of range [1, " + std::to_string(ECO_MAX_SPINS) + "]");
   if (c->max_steps < 1 || c->max_steps > 32767) return fail(ECO_ERR_ARG, "max_steps out of range [1, 32767]");
-  if (c->n_obs < 1 || c->n_obs > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs out of range [1, 8]");
+  if (c->n_obs < 1 || c->n_obs > 13) return fail(ECO_ERR_ARG, "n_obs out of range [1, 13]");
   if (c->obs_ids[0] != ECO_OBS_SPIN_STATE)
     return fail(ECO_ERR_OBSERVABLE, "First observable must be Observation.SPIN_STATE.");
-  for (int i = 0; i < c->n_obs; ++i)
-    if (c->obs_ids[i] < 1 || c->obs_ids[i] > 13) return fail(ECO_ERR_ARG, "unknown observable id");
+  const int t = c->optimisation_target;
+  if (t < ECO_TARGET_CUT || t > ECO_TARGET_MIN_DOM_SET || t == ECO_TARGET_ENERGY)
+    return fail(ECO_ERR_TARGET, "Invalid optimization target: " + std::to_string(t) + " and biased False");
+  for (int i = 0; i < c->n_obs; ++i) {
+    const int id = c->obs_ids[i];
+    if (id < 1 || id > 13) return fail(ECO_ERR_ARG, "unknown observable id");
+    if ((t == ECO_TARGET_CUT || t == ECO_TARGET_MIN_CUT) &&
+        (id == ECO_OBS_IMMEDIATE_VALIDITY_DIFFERENCE || id == ECO_OBS_IMMEDIATE_VALIDITY_CHANGE ||
+         id == ECO_OBS_NUMBER_OF_VALIDITY_IMPROVEMENTS))
+      return fail(ECO_ERR_OBSERVABLE, "validity-mask observables are undefined for cut targets (the "
+                                      "reference's scorer returns a list: TypeError)");
+  }
   if (c->spin_basis != ECO_BASIS_SIGNED && c->spin_basis != ECO_BASIS_BINARY)
     return fail(ECO_ERR_BASIS, "Unrecognised SpinBasis");
   if (c->horizon_length < 1) return fail(ECO_ERR_ARG, "horizon_length must be >= 1");
@@ -519,15 +480,7 @@ static int check_err_word(int32_t* w, hipStream_t st) {
   return ECO_OK;
 }
 
-#define ECO_DISPATCH_VPT(N, CALL)                                   \
-  do {                                                              \
-    if ((N) <= 64) { constexpr int V = 1; CALL; }                   \
-    else if ((N) <= 128) { constexpr int V = 2; CALL; }             \
-    else if ((N) <= 256) { constexpr int V = 4; CALL; }             \
-    else if ((N) <= 512) { constexpr int V = 8; CALL; }             \
-    else if ((N) <= 1024) { constexpr int V = 16; CALL; }           \
-    else { constexpr int V = 32; CALL; }                            \
-  } while (0)
+static inline bool generic_target(const eco_env_config* c) { return c->optimisation_target != ECO_TARGET_CUT; }
 
 }  // namespace eco
 
@@ -591,6 +544,7 @@ extern "C" int eco_env_reset(const eco_env_config* cfg, const eco_graph_set* gs,
   build_time_table_kernel<<<1, 1, 0, st>>>(a.state, a.L.off_tab, cfg->max_steps);
   const int blocks = (batch + 3) / 4;
   const size_t lds = (size_t)4 * cfg->n_spins;
+  if (generic_target(cfg)) return env_reset_problem_launch(a, blocks, lds, st);
   ECO_DISPATCH_VPT(cfg->n_spins, (env_reset_kernel<V><<<blocks, 256, lds, st>>>(a)));
   return check_launch("env_reset");
 }
@@ -612,18 +566,23 @@ extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, 
   a.actions = actions; a.rewards = rewards; a.dones = dones; a.obs_x = obs_x; a.obs_f64 = obs_f64;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (batch + 3) / 4;
+  if (generic_target(cfg)) return env_step_problem_launch(a, blocks, (size_t)4 * cfg->n_spins, st);
   ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, 0, st>>>(a)));
   return check_launch("env_step");
 }
 
-extern "C" int eco_env_greedy_actions(const eco_env_config* cfg, void* state, int32_t batch, int32_t* actions,
-                                      eco_stream_t stream) {
+extern "C" int eco_env_greedy_actions(const eco_env_config* cfg, const eco_graph_set* gs, void* state,
+                                      int32_t batch, int32_t* actions, eco_stream_t stream) {
   EnvArgs a;
-  int rc = make_args(a, cfg, nullptr, state, batch);
+  int rc = make_args(a, cfg, gs, state, batch);
   if (rc) return rc;
   if (!actions) return fail(ECO_ERR_ARG, "null actions");
+  if (cfg->optimisation_target == ECO_TARGET_MIN_DOM_SET && !gs)
+    return fail(ECO_ERR_ARG, "MIN_DOM_SET greedy actions need the graph set");
   const int blocks = (batch + 3) / 4;
-  ECO_DISPATCH_VPT(cfg->n_spins, (env_greedy_kernel<V><<<blocks, 256, 0, (hipStream_t)stream>>>(a, actions)));
+  hipStream_t st = (hipStream_t)stream;
+  if (generic_target(cfg)) return env_greedy_problem_launch(a, actions, blocks, (size_t)4 * cfg->n_spins, st);
+  ECO_DISPATCH_VPT(cfg->n_spins, (env_greedy_kernel<V><<<blocks, 256, 0, st>>>(a, actions)));
   return check_launch("env_greedy");
 }
 

@@ -1,0 +1,108 @@
+// Device-side pieces shared by the batched env kernels: the MaxCut kernels (eco_env.hip) and the
+// generic-scorer kernels (eco_env_problems.hip).
+#pragma once
+#include "eco_common.h"
+
+namespace eco {
+
+struct EnvArgs {
+  eco_env_config cfg;
+  eco_graph_set gs;
+  EnvLayout L;
+  uint8_t* state;
+  int B;
+  const int32_t* graph_ids;
+  const int8_t* spins_in;
+  const uint8_t* mask;
+  uint64_t seed;
+  const int32_t* actions;
+  double* rewards;
+  uint8_t* dones;
+  float* obs_x;
+  double* obs_f64;
+  int32_t* err;  // device error word (first error wins)
+};
+
+__device__ __forceinline__ EpScal* scal_ptr(const EnvArgs& a) { return (EpScal*)(a.state + a.L.off_scal); }
+__device__ __forceinline__ const double* tab_ptr(const EnvArgs& a) { return (const double*)(a.state + a.L.off_tab + 256); }
+
+// one node's fp32 feature row: ECO_OBS_X_STRIDE(nobs) floats (8, or 16 beyond 8 observables)
+__device__ __forceinline__ void store_obs_row(float* obs_x, size_t row, int nobs, const float (&xf)[ECO_MAX_OBS]) {
+  if (nobs <= 8) {
+    float4* dst = (float4*)(obs_x + row * 8);
+    dst[0] = make_float4(xf[0], xf[1], xf[2], xf[3]);
+    dst[1] = make_float4(xf[4], xf[5], xf[6], xf[7]);
+  } else {
+    float4* dst = (float4*)(obs_x + row * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = make_float4(xf[4 * i], xf[4 * i + 1], xf[4 * i + 2], xf[4 * i + 3]);
+  }
+}
+
+// LDS written by a wave and read back by the same wave only: a wave-scope fence suffices
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// HistoryBuffer.update (src/envs/utils.py:438-464): is the flipped-vertex set after flipping `act` new?
+// The set is identified by the spin configuration (words = ballot(s > 0) per 64 vertices); a Zobrist
+// hash of the set indexes an open-addressing table of the episode's visited configurations.  The
+// initial (empty) set is never inserted, as in the reference.
+template <int VPT>
+__device__ __forceinline__ bool history_update(const EnvArgs& a, int e, int lane, EpScal* sc, int act,
+                                               const uint64_t (&words)[VPT]) {
+  const EnvLayout& L = a.L;
+  const int T = a.cfg.max_steps;
+  const uint64_t hash = sc->hash ^ zobrist(act);
+  const int cap = L.cap;
+  const int W = L.words;
+  uint32_t* vidx = (uint32_t*)(a.state + L.off_vidx) + (size_t)e * cap;
+  uint64_t* vh = (uint64_t*)(a.state + L.off_vhash) + (size_t)e * cap;
+  uint64_t* vst = (uint64_t*)(a.state + L.off_vstates) + (size_t)e * (T + 1) * W;
+  bool isnew = true;
+  int slot = (int)(hash & (uint64_t)(cap - 1));
+  for (;;) {
+    const uint32_t id = vidx[slot];
+    if (id == 0u) break;
+    if (vh[slot] == hash) {
+      bool same = true;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) same = same && (k >= W || vst[(size_t)(id - 1) * W + k] == words[k]);
+      if (same) { isnew = false; break; }
+    }
+    slot = (slot + 1) & (cap - 1);
+  }
+  if (lane == 0) {
+    sc->hash = hash;
+    if (isnew) {
+      const int n = sc->visit_count;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k)
+        if (k < W) vst[(size_t)n * W + k] = words[k];  // VPT = next power of two >= W
+      vh[slot] = hash;
+      vidx[slot] = (uint32_t)(n + 1);
+      sc->visit_count = n + 1;
+    }
+  }
+  return isnew;
+}
+
+// vertices per lane for N spins (one 64-lane wave per episode)
+#define ECO_DISPATCH_VPT(N, CALL)                                   \
+  do {                                                              \
+    if ((N) <= 64) { constexpr int V = 1; CALL; }                   \
+    else if ((N) <= 128) { constexpr int V = 2; CALL; }             \
+    else if ((N) <= 256) { constexpr int V = 4; CALL; }             \
+    else if ((N) <= 512) { constexpr int V = 8; CALL; }             \
+    else if ((N) <= 1024) { constexpr int V = 16; CALL; }           \
+    else { constexpr int V = 32; CALL; }                            \
+  } while (0)
+
+// generic-scorer launches (eco_env_problems.hip): 4 episodes per 256-thread block, lds = 4 N bytes
+int env_reset_problem_launch(const EnvArgs& a, int blocks, size_t lds, hipStream_t st);
+int env_step_problem_launch(const EnvArgs& a, int blocks, size_t lds, hipStream_t st);
+int env_greedy_problem_launch(const EnvArgs& a, int32_t* actions, int blocks, size_t lds, hipStream_t st);
+
+}  // namespace eco

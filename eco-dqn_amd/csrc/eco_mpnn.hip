@@ -908,7 +908,7 @@ __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, 
 static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
                    const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope) {
   if (!packed || !gs || !graph_ids || !obs_x) return fail(ECO_ERR_ARG, "null argument");
-  if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
+  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
   if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
   const int N = gs->n_spins;
   if (N < 1 || N > MPNN_MAX_SPINS_LARGE) return fail(ECO_ERR_ARG, "mpnn supports 1 <= N <= 2048");
@@ -933,7 +933,7 @@ extern "C" int eco_debug_phase_ts(unsigned long long* host, int32_t n) {
 #endif
 
 extern "C" size_t eco_mpnn_param_count(int32_t n_obs_in) {
-  if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return 0;
+  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return 0;
   return (size_t)flat_offsets(n_obs_in).total;
 }
 
@@ -941,7 +941,7 @@ extern "C" size_t eco_mpnn_packed_count(void) { return (size_t)PK_TOTAL; }
 
 extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packed, eco_stream_t stream) {
   if (!params || !packed) return fail(ECO_ERR_ARG, "null params/packed");
-  if (n_obs_in < 1 || n_obs_in > ECO_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
+  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
   pack_kernel<<<(PK_TOTAL + 255) / 256, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   return check_launch("mpnn_pack");
 }

@@ -18,7 +18,16 @@ lib = ctypes.CDLL(LIB_PATH)
 # ---- status codes / enums (eco_hip.h) ----
 ECO_OK, ECO_ERR_ARG, ECO_ERR_HIP, ECO_ERR_PAST_END, ECO_ERR_BASIS, ECO_ERR_TARGET, ECO_ERR_OBSERVABLE, \
     ECO_ERR_GRAPH = range(8)
-ECO_MAX_OBS = 8
+ECO_MAX_OBS = 16          # observables per env (MAIN_OBSERVABLES has 13)
+ECO_MPNN_MAX_OBS = 8      # MPNN n_obs_in limit (node-feature rows of 8 floats)
+ECO_ENV_SCALARS = 16
+ECO_TARGET_CUT, ECO_TARGET_ENERGY, ECO_TARGET_MIN_COVER, ECO_TARGET_MIN_CUT, ECO_TARGET_MAX_IND_SET, \
+    ECO_TARGET_MAX_CLIQUE, ECO_TARGET_MIN_DOM_SET = range(1, 8)
+
+
+def obs_x_stride(n_obs):
+    """ECO_OBS_X_STRIDE: floats per node-feature row of obs_x."""
+    return 8 if n_obs <= 8 else 16
 ECO_MAX_SPINS = 2048
 ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL = 0, 1
 ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
@@ -30,7 +39,8 @@ class EnvConfig(ctypes.Structure):
                 ("norm_rewards", ctypes.c_int32), ("reversible_spins", ctypes.c_int32),
                 ("spin_basis", ctypes.c_int32), ("stopping", ctypes.c_int32),
                 ("has_basin_reward", ctypes.c_int32), ("has_stag_punishment", ctypes.c_int32),
-                ("horizon_length", ctypes.c_int32), ("basin_reward", ctypes.c_double),
+                ("horizon_length", ctypes.c_int32), ("optimisation_target", ctypes.c_int32),
+                ("basin_reward", ctypes.c_double),
                 ("stag_punishment", ctypes.c_double)]
 
 
@@ -67,7 +77,8 @@ _SIG = {
                                     _P, _P]),
     "eco_env_read": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P, _P, _P]),
     "eco_check_errors": (ctypes.c_int, [_P]),
-    "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P]),
+    "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), ctypes.POINTER(GraphSet), _P, _I, _P,
+                                              _P]),
     "eco_mpnn_param_count": (ctypes.c_size_t, [_I]),
     "eco_mpnn_packed_count": (ctypes.c_size_t, []),
     "eco_mpnn_pack": (ctypes.c_int, [_P, _I, _P, _P]),

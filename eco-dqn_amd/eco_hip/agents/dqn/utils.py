@@ -44,8 +44,8 @@ class ReplayBuffer:
         self.n_spins = n_spins
         dev = torch.device(device)
         self.device = dev
-        self.xs = torch.zeros(capacity, n_spins, _lib.ECO_MAX_OBS, dtype=torch.float32, device=dev)
-        self.xn = torch.zeros(capacity, n_spins, _lib.ECO_MAX_OBS, dtype=torch.float32, device=dev)
+        self.xs = torch.zeros(capacity, n_spins, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=dev)
+        self.xn = torch.zeros(capacity, n_spins, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=dev)
         self.gid = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.act = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.rew = torch.zeros(capacity, dtype=torch.float32, device=dev)
@@ -70,8 +70,8 @@ class ReplayBuffer:
     def _buffers(self, m):
         if m not in self._out:
             dev = self.device
-            self._out[m] = (torch.empty(m, self.n_spins, _lib.ECO_MAX_OBS, device=dev),
-                            torch.empty(m, self.n_spins, _lib.ECO_MAX_OBS, device=dev),
+            self._out[m] = (torch.empty(m, self.n_spins, _lib.ECO_MPNN_MAX_OBS, device=dev),
+                            torch.empty(m, self.n_spins, _lib.ECO_MPNN_MAX_OBS, device=dev),
                             torch.empty(m, dtype=torch.int32, device=dev), torch.empty(m, dtype=torch.int32, device=dev),
                             torch.empty(m, device=dev), torch.empty(m, device=dev))
         return self._out[m]

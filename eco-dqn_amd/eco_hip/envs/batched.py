@@ -1,4 +1,4 @@
-"""Batched MaxCut SpinSystem: B concurrent episodes on one GPU (libecohip env kernels).
+"""Batched SpinSystem: B concurrent episodes on one GPU (libecohip env kernels).
 
 The reference steps one `SpinSystemBase` at a time from a Python loop
 (dqn.py:273-327, experiments/utils.py:169-201).  `VecSpinSystem` holds B episodes
@@ -21,10 +21,9 @@ def make_config(n_spins, max_steps, observables=DEFAULT_OBSERVABLES, reward_sign
                 stag_punishment=None, basin_reward=None, reversible_spins=True, stopping=Stopping.NORMAL,
                 **_ignored):
     """env_args (spinsystem.py:29-48 defaults) -> eco_env_config."""
-    if optimisation_target != OptimisationTarget.CUT:
-        # the reference factory has no ENERGY branch (score_solver.py:866-885); other
-        # problems are off the MaxCut hot path
-        raise NotImplementedError(f"Invalid optimization target: {optimisation_target} (eco_hip runs CUT only)")
+    if optimisation_target == OptimisationTarget.ENERGY:
+        # the reference factory has no ENERGY branch (score_solver.py:866-885)
+        raise NotImplementedError(f"Invalid optimization target: {optimisation_target} and biased False")
     if extra_action != ExtraAction.NONE:
         raise NotImplementedError("eco_hip runs ExtraAction.NONE only (PASS shape-breaks the reference "
                                   "score mask, spinsystem.py:141-142,393)")
@@ -32,8 +31,14 @@ def make_config(n_spins, max_steps, observables=DEFAULT_OBSERVABLES, reward_sign
         raise NotImplementedError("finite memory_length is not on the hot path")
     obs = list(observables)
     assert obs[0] == Observable.SPIN_STATE, "First observable must be Observation.SPIN_STATE."
-    if len(obs) > _lib.ECO_MAX_OBS:
-        raise ValueError("at most 8 observables")
+    if len(obs) > 13:
+        raise ValueError("at most 13 observables")
+    if optimisation_target in (OptimisationTarget.CUT, OptimisationTarget.MIN_CUT) and any(
+            o in (Observable.IMMEDIATE_VALIDITY_DIFFERENCE, Observable.IMMEDIATE_VALIDITY_CHANGE,
+                  Observable.NUMBER_OF_VALIDITY_IMPROVEMENTS) for o in obs):
+        # the cut scorers return the invalidity mask as a python list (score_solver.py:403-407, :489-493)
+        raise TypeError("unsupported operand type(s) for /: 'list' and 'int' (validity-mask observable "
+                        "with a cut target)")
     if spin_basis not in (SpinBasis.SIGNED, SpinBasis.BINARY):
         raise Exception("Unrecognised SpinBasis")
     c = _lib.EnvConfig()
@@ -52,16 +57,17 @@ def make_config(n_spins, max_steps, observables=DEFAULT_OBSERVABLES, reward_sign
     c.has_stag_punishment = int(stag_punishment is not None)
     c.stag_punishment = float(stag_punishment) if stag_punishment is not None else 0.0
     c.horizon_length = int(horizon_length if horizon_length is not None else max_steps)
+    c.optimisation_target = optimisation_target.value
     return c
 
 
 class VecSpinSystem:
-    """B MaxCut episodes over graphs of a GraphStore.
+    """B episodes over graphs of a GraphStore, for any OptimisationTarget scorer except ENERGY.
 
     reset(graph_ids, spins=None, mask=None, seed=0) and step(actions) return the
-    fp32 node features obs_x [B, N, 8] that the MPNN consumes (obs.float() of the
-    reference observation rows, dqn.py:282); pass want_f64=True to also fill
-    obs_f64 [B, n_obs, N] (the reference's float64 rows, for parity checks)."""
+    fp32 node features obs_x [B, N, W] (W = 8, or 16 beyond 8 observables) that the MPNN
+    consumes (obs.float() of the reference observation rows, dqn.py:282); pass want_f64=True
+    to also fill obs_f64 [B, n_obs, N] (the reference's float64 rows, for parity checks)."""
 
     def __init__(self, graphs, n_envs, max_steps, want_f64=False, stream=None, **env_args):
         self.graphs = graphs
@@ -78,13 +84,14 @@ class VecSpinSystem:
         if nbytes == 0:
             raise ValueError(_lib.last_error())
         self.state = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-        self.obs_x = torch.zeros(n_envs, self.n_spins, _lib.ECO_MAX_OBS, dtype=torch.float32, device=dev)
+        self.obs_x = torch.zeros(n_envs, self.n_spins, _lib.obs_x_stride(self.n_obs), dtype=torch.float32,
+                                 device=dev)
         self.obs_f64 = (torch.zeros(n_envs, self.n_obs, self.n_spins, dtype=torch.float64, device=dev)
                         if want_f64 else None)
         self.rewards = torch.zeros(n_envs, dtype=torch.float64, device=dev)
         self.dones = torch.zeros(n_envs, dtype=torch.uint8, device=dev)
         self.graph_ids = torch.zeros(n_envs, dtype=torch.int32, device=dev)
-        self.scalars = torch.zeros(n_envs, 8, dtype=torch.float64, device=dev)
+        self.scalars = torch.zeros(n_envs, _lib.ECO_ENV_SCALARS, dtype=torch.float64, device=dev)
         self.stream = stream
 
     def _s(self):
@@ -130,12 +137,12 @@ class VecSpinSystem:
         return self.obs_x, self.rewards, self.dones
 
     def greedy_actions(self, actions_out=None):
-        """Greedy solver step (solver.py:100-131): argmax of the immediate cut change per episode;
+        """Greedy solver step (solver.py:100-131): argmax of the scorer's score mask per episode;
         episodes without a non-negative change are marked done."""
         out = actions_out if actions_out is not None else torch.empty(self.n_envs, dtype=torch.int32,
                                                                       device=self.graphs.device)
-        _lib.check(_lib.lib.eco_env_greedy_actions(ctypes.byref(self.cfg), _lib.ptr(self.state), self.n_envs,
-                                                   _lib.ptr(out), self._s()))
+        _lib.check(_lib.lib.eco_env_greedy_actions(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
+                                                   _lib.ptr(self.state), self.n_envs, _lib.ptr(out), self._s()))
         return out
 
     def check_errors(self):
@@ -150,7 +157,9 @@ class VecSpinSystem:
                                          _lib.ptr(self.scalars), _lib.ptr(sp), _lib.ptr(bs), self._s()))
         s = self.scalars
         out = dict(current_step=s[:, 0], score=s[:, 1], normalized_score=s[:, 2], best_score=s[:, 3],
-                   best_score_normalized=s[:, 4], best_solution=s[:, 5], hamming=s[:, 6], done=s[:, 7])
+                   best_score_normalized=s[:, 4], best_solution=s[:, 5], hamming=s[:, 6], done=s[:, 7],
+                   max_local_reward=s[:, 8], quality_normalizer=s[:, 9], invalidity_normalizer=s[:, 10],
+                   lower_bound=s[:, 11], set_size=s[:, 12], invalidity=s[:, 13])
         if spins:
             out["spins"] = sp
         if best_spins:

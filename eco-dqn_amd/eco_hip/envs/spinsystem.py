@@ -20,21 +20,31 @@ from .utils import (DEFAULT_OBSERVABLES, EdgeType, ExtraAction, GraphGenerator, 
 ActionResult = namedtuple("action_result", ("snapshot", "observation", "reward", "is_done", "info"))
 
 
-class MaximumCutScorer:
-    """Host-side view of MaximumCutUnbiasedScorer (score_solver.py:343-419): the normalisers the
-    device computed, plus numpy score helpers for callers such as the Greedy baseline."""
+class DeviceScorer:
+    """Host-side view of the env's ScoreSolver (score_solver.py:11-172): the normalisers the device computed
+    for the current graph (read back after every call).  For the cut targets it also offers the numpy score
+    helpers callers such as the reference's Greedy solver use; the set problems' masks live on the device
+    only (VecSpinSystem.greedy_actions evaluates them there)."""
 
-    def __init__(self, meta):
-        self._max_local_reward = float(meta[0])
-        self._solution_quality_normalizer = float(meta[1])
-        self._lower_bound = float(meta[2])
-        self._invalidity_normalizer = 1
+    def __init__(self, target, scalars):
+        self.target = target
+        self._max_local_reward = float(scalars["max_local_reward"])
+        self._solution_quality_normalizer = float(scalars["quality_normalizer"])
+        self._invalidity_normalizer = float(scalars["invalidity_normalizer"])
+        self._lower_bound = float(scalars["lower_bound"])
 
-    @staticmethod
-    def get_solution(spins, matrix):
+    def _cut_only(self):
+        if self.target not in (OptimisationTarget.CUT, OptimisationTarget.MIN_CUT):
+            raise NotImplementedError(f"{self.target}: scorer masks are evaluated on the device "
+                                      "(VecSpinSystem.greedy_actions / obs rows)")
+
+    def get_solution(self, spins, matrix):
+        self._cut_only()
         return (1 / 4) * np.sum(np.multiply(matrix, 1 - np.outer(spins, spins)))
 
     def get_solution_quality(self, spins, matrix):
+        if self.target == OptimisationTarget.MIN_CUT:
+            return max(0, self._solution_quality_normalizer) - self.get_solution(spins, matrix)
         return self.get_solution(spins, matrix) + abs(min(0, self._lower_bound))
 
     get_score = get_solution_quality
@@ -42,17 +52,15 @@ class MaximumCutScorer:
     def get_normalized_score(self, spins, matrix):
         return self.get_solution_quality(spins, matrix) / self._solution_quality_normalizer
 
-    @staticmethod
-    def get_score_mask(spins, matrix):
-        return spins * (matrix @ spins)
+    def get_score_mask(self, spins, matrix):
+        self._cut_only()
+        g = spins * (matrix @ spins)
+        return g if self.target == OptimisationTarget.CUT else -g
 
     get_solution_quality_mask = get_score_mask
 
     def get_normalized_score_mask(self, spins, matrix):
         return self.get_score_mask(spins, matrix) / self._solution_quality_normalizer
-
-    def is_valid(self, spins, matrix):
-        return True
 
 
 class SpinSystemFactory:
@@ -124,13 +132,18 @@ class SpinSystemBase:
         key = id(matrix)
         if key != self._matrix_key or self._vec is None:
             store = GraphStore.from_dense([np.asarray(matrix, dtype=np.float64)], device=self.device)
-            self._vec = VecSpinSystem(store, 1, self.max_steps, want_f64=True, **self._env_args)
+            if self._vec is None:
+                self._vec = VecSpinSystem(store, 1, self.max_steps, want_f64=True, **self._env_args)
+            else:  # same episode state: the scorer's normalisers carry over like the reference's (:216-219)
+                self._vec.graphs = store
             self._matrix_key = key
         self.matrix = matrix
         self.matrix_obs = matrix
 
     def _sync(self):
         st = self._vec.read(spins=True, best_spins=True)
+        self.scorer = DeviceScorer(self.optimisation_target, {k: v[0].item() for k, v in st.items()
+                                                              if k not in ("spins", "best_spins")})
         self.current_step = int(st["current_step"][0].item())
         self.score = float(st["score"][0].item())
         self.normalized_score = float(st["normalized_score"][0].item())
@@ -165,7 +178,8 @@ class SpinSystemBase:
         for _ in range(1000):
             matrix = self.gg.get()
             self._bind_graph(matrix)
-            if int(self._vec.graphs.valid[0].item()):
+            cut_like = self.optimisation_target in (OptimisationTarget.CUT, OptimisationTarget.MIN_CUT)
+            if not cut_like or int(self._vec.graphs.valid[0].item()):  # set problems: never redrawn
                 break
         else:
             raise ValueError("graph generator keeps returning graphs with no nonzero local reward")
@@ -178,7 +192,6 @@ class SpinSystemBase:
             sp = self._format_spins_to_signed(spins)
         self._vec.reset(graph_ids=[0], spins=np.asarray(sp)[None])
         self._vec.check_errors()
-        self.scorer = MaximumCutScorer(self._vec.graphs.meta[0].cpu().numpy())
         self._sync()
         self.solution = self.best_solution
         return self.get_observation()

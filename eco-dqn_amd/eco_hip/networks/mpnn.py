@@ -40,7 +40,7 @@ class MPNN(torch.nn.Module):
         if n_layers != 3 or n_features != N_FEATURES or tied_weights or list(n_hid_readout):
             raise NotImplementedError("eco_hip implements the ECO-DQN MPNN configuration used by the "
                                       "reference (n_layers=3, n_features=64, untied, no hidden readout)")
-        if not 1 <= n_obs_in <= _lib.ECO_MAX_OBS:
+        if not 1 <= n_obs_in <= _lib.ECO_MPNN_MAX_OBS:
             raise ValueError("n_obs_in must be in [1, 8]")
         self.n_obs_in = n_obs_in
         self.n_layers = n_layers
@@ -168,7 +168,7 @@ class MPNN(torch.nn.Module):
             view = obs
         B, R, N = view.shape
         k = self.n_obs_in
-        x = torch.zeros(B, N, _lib.ECO_MAX_OBS, dtype=torch.float32, device=self.flat.device)
+        x = torch.zeros(B, N, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=self.flat.device)
         x[:, :, :k] = view[:, :k, :].transpose(1, 2).to(x.device, torch.float32)
         adj = view[:, k:, :].detach().cpu().numpy()
         store = GraphStore(*dense_to_csr([a.T for a in adj]), device=self.flat.device)

@@ -54,17 +54,26 @@ enum { ECO_OBS_SPIN_STATE = 1, ECO_OBS_IMMEDIATE_QUALITY_CHANGE = 2, ECO_OBS_IMM
 enum { ECO_REWARD_DENSE = 1, ECO_REWARD_BLS = 2, ECO_REWARD_SINGLE = 3, ECO_REWARD_CUSTOM_BLS = 4 };
 enum { ECO_BASIS_SIGNED = 1, ECO_BASIS_BINARY = 2 };
 enum { ECO_STOP_NORMAL = 1, ECO_STOP_QUARTER = 2, ECO_STOP_EARLY = 3 };
+/* OptimisationTarget (src/envs/utils.py:32-39); ENERGY has no scorer (score_solver.py:860-885) */
+enum { ECO_TARGET_CUT = 1, ECO_TARGET_ENERGY = 2, ECO_TARGET_MIN_COVER = 3, ECO_TARGET_MIN_CUT = 4,
+       ECO_TARGET_MAX_IND_SET = 5, ECO_TARGET_MAX_CLIQUE = 6, ECO_TARGET_MIN_DOM_SET = 7 };
 
-#define ECO_MAX_OBS 8      /* observables per node (obs_x rows are padded to 8 floats) */
+#define ECO_MAX_OBS 16     /* observables per env (all 13 of MAIN_OBSERVABLES, src/envs/utils.py:76-88) */
+#define ECO_MPNN_MAX_OBS 8 /* MPNN n_obs_in limit (its node-feature rows are 8 floats) */
+/* obs_x row width in floats for n_obs observables: 8 up to 8 observables, else 16 */
+#define ECO_OBS_X_STRIDE(n_obs) ((n_obs) <= 8 ? 8 : 16)
 #define ECO_MAX_SPINS 2048 /* largest N the env kernels take (wave-per-episode, 32 vertices per lane) */
 
 /* Env configuration: the kwargs of core.make("SpinSystem", gg, max_steps, **env_args)
- * (src/envs/core.py:3-10 -> spinsystem.py:29-48).  Only OptimisationTarget.CUT,
- * unbiased graphs, ExtraAction.NONE and memory_length=None are on the hot path. */
+ * (src/envs/core.py:3-10 -> spinsystem.py:29-48).  OptimisationTarget.CUT is the hot path (its own
+ * kernels); MIN_COVER, MIN_CUT, MAX_IND_SET, MAX_CLIQUE and MIN_DOM_SET run the generic scorer kernels
+ * (score_solver.py:232-858).  Unbiased graphs, ExtraAction.NONE and memory_length=None only.
+ * With CUT / MIN_CUT the validity-mask observables (3, 4, 9) are rejected with ECO_ERR_OBSERVABLE:
+ * those scorers return the invalidity mask as a python list and the reference raises TypeError. */
 typedef struct {
   int32_t n_spins;                /* N */
   int32_t max_steps;              /* T */
-  int32_t n_obs;                  /* number of observables, 1..8 */
+  int32_t n_obs;                  /* number of observables, 1..13 */
   int32_t obs_ids[ECO_MAX_OBS];   /* Observable values; obs_ids[0] == SPIN_STATE */
   int32_t reward_signal;          /* ECO_REWARD_* */
   int32_t norm_rewards;           /* bool */
@@ -74,6 +83,7 @@ typedef struct {
   int32_t has_basin_reward;       /* basin_reward is not None */
   int32_t has_stag_punishment;    /* stag_punishment is not None */
   int32_t horizon_length;         /* horizon_length, or max_steps when None (spinsystem.py:163) */
+  int32_t optimisation_target;    /* ECO_TARGET_* */
   double basin_reward;
   double stag_punishment;
 } eco_env_config;
@@ -131,8 +141,11 @@ size_t eco_env_state_bytes(const eco_env_config *cfg, int32_t batch);
  * NULL draws uniform +-1 spins from a counter-based generator keyed by
  * (seed, episode) (reversible) or all -1 (irreversible, :295-297).
  * reset_mask[B] or NULL (= all): only episodes with mask != 0 are reset.
- * `state` must be zero-filled before its first reset.
- * Outputs (each may be NULL): obs_x[B][N][8] fp32 node features as the MPNN reads
+ * `state` must be zero-filled before its first reset.  As in the reference, the first observation
+ * after a reset divides the validity difference by the invalidity normaliser of the episode's
+ * previous reset (set_invalidity_normalizer runs after _reset_state, spinsystem.py:216-219), 1 for
+ * the first reset of a zero-filled state.
+ * Outputs (each may be NULL): obs_x[B][N][ECO_OBS_X_STRIDE(n_obs)] fp32 node features as the MPNN reads
  * them (obs.float(), dqn.py:282), obs_f64[B][n_obs][N] the reference's float64
  * observation rows (get_observation :561-574 without the appended adjacency). */
 int eco_env_reset(const eco_env_config *cfg, const eco_graph_set *gs, void *state, int32_t batch,
@@ -145,16 +158,20 @@ int eco_env_step(const eco_env_config *cfg, const eco_graph_set *gs, void *state
                  const int32_t *actions, double *rewards, uint8_t *dones, float *obs_x, double *obs_f64,
                  eco_stream_t stream);
 
-/* Greedy solver (src/agents/solver.py:88-131) for every episode: actions[B] = argmax of the
- * immediate cut change (allowed vertices only when irreversible); episodes with no
- * non-negative change are marked done (the solver stops). Step with eco_env_step. */
-int eco_env_greedy_actions(const eco_env_config *cfg, void *state, int32_t batch, int32_t *actions,
-                           eco_stream_t stream);
+/* Greedy solver (src/agents/solver.py:88-131) for every episode: actions[B] = argmax (first index) of
+ * the scorer's score mask (allowed vertices only when irreversible); episodes with no non-negative
+ * change are marked done (the solver stops). Step with eco_env_step.  `gs` is the set the episodes
+ * were reset on (read by MIN_DOM_SET's neighbour counts; may be NULL for the other targets). */
+int eco_env_greedy_actions(const eco_env_config *cfg, const eco_graph_set *gs, void *state, int32_t batch,
+                           int32_t *actions, eco_stream_t stream);
 
 /* Read-out of the env attributes callers use (dqn.py:564-566, experiments/utils.py:194-197):
- * scalars[B][8] = {current_step, score, normalized_score, best_score,
- *                  best_score_normalized, best_solution, hamming_to_best, done};
+ * scalars[B][ECO_ENV_SCALARS] = {current_step, score, normalized_score, best_score,
+ *     best_score_normalized, best_solution, hamming_to_best, done, max_local_reward,
+ *     solution_quality_normalizer, invalidity_normalizer, lower_bound, set_size (#spins == +1),
+ *     invalidity_degree, graph_id, 0};
  * spins / best_spins [B][N] int8 signed (each may be NULL). */
+#define ECO_ENV_SCALARS 16
 int eco_env_read(const eco_env_config *cfg, const void *state, int32_t batch, double *scalars, int8_t *spins,
                  int8_t *best_spins, eco_stream_t stream);
 

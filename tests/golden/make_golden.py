@@ -346,10 +346,108 @@ def make_greedy_solver():
     np.savez_compressed(os.path.join(HERE, "greedy_solver.npz"), **out)
 
 
+PROBLEMS = (("MIN_COVER", "uniform"), ("MAX_IND_SET", "uniform"), ("MAX_CLIQUE", "uniform"),
+            ("MIN_DOM_SET", "uniform"), ("MIN_CUT", "discrete"), ("CUT", "uniform"))
+MAIN_OBS = [Observable(v) for v in range(1, 14)]   # src/envs/utils.py:76-88
+
+
+def problem_args(target, mode, n):
+    """experiments/train_eco.py:244-315: MAIN_OBSERVABLES for the set problems, DEFAULT_OBSERVABLES for the
+    cut problems (the validity-mask observables raise TypeError with a cut scorer); s2v as :311-315."""
+    a = env_args("eco", n)
+    a["optimisation_target"] = OptimisationTarget[target]
+    if target not in ("CUT", "MIN_CUT"):
+        a["observables"] = MAIN_OBS
+    if mode == "s2v":
+        a.update(observables=[Observable.SPIN_STATE], reversible_spins=False, basin_reward=None,
+                 reward_signal=RewardSignal.DENSE)
+    return a
+
+
+def make_env_problems():
+    """Every OptimisationTarget scorer (score_solver.py:232-858) through the reference env.  Each case's env
+    is built on graph J0 (the constructor draws once, :154, and resets once, :168) and then reset onto graph J with
+    the recorded spins, so the stale invalidity normaliser of the first observation (set only after
+    _reset_state, :216-219) comes from J0.  A greedy rollout (solver.py:110-127 rule on the scorer's score
+    mask) from the same start is recorded as well."""
+    from src.envs.utils import SetGraphGenerator
+    rng = np.random.default_rng(77)
+    out = {}
+    ci = 0
+    for target, w in PROBLEMS:
+        for mode in ("eco", "s2v"):
+            for n, p in ((20, 0.15), (24, 0.35)):
+                J0 = graphs.er_graph(n, p, rng, w)
+                J = graphs.er_graph(n, p, rng, w)
+                T = 2 * n if mode == "eco" else n
+                env = ising_env.make("SpinSystem", SetGraphGenerator([J0, J0, J], ordered=True), T,
+                                     **problem_args(target, mode, n))
+                if mode == "s2v":
+                    spins = -np.ones(n, dtype=np.int64)
+                    actions = rng.permutation(n)
+                else:
+                    spins = 2 * rng.integers(0, 2, n) - 1
+                    actions = rng.integers(0, n, T)
+                n_obs = len(env.observables)
+                obs = env.reset(spins=spins)
+                assert np.array_equal(env.matrix, J)
+                sc = env.scorer
+                rec = dict(obs=[obs[:n_obs].copy()], rew=[], done=[], score=[env.score], nscore=[env.normalized_score],
+                           best_score=[env.best_score], best_nscore=[env.best_score_normalized],
+                           best_solution=[env.best_solution])
+                norms = [sc._max_local_reward, sc._solution_quality_normalizer, sc._invalidity_normalizer,
+                         sc._lower_bound]
+                for a in actions:
+                    obs, rew, done, _ = env.step(int(a))
+                    rec["obs"].append(obs[:n_obs].copy())
+                    rec["rew"].append(float(rew))
+                    rec["done"].append(bool(done))
+                    for k, v in (("score", env.score), ("nscore", env.normalized_score),
+                                 ("best_score", env.best_score), ("best_nscore", env.best_score_normalized),
+                                 ("best_solution", env.best_solution)):
+                        rec[k].append(v)
+                    if done:
+                        break
+                # greedy rollout from the same start on the same graph
+                genv = ising_env.make("SpinSystem", SingleGraphGenerator(J), T, **problem_args(target, mode, n))
+                genv.reset(spins=spins)
+                gacts, gdone = [], False
+                while not gdone:
+                    mask = genv.scorer.get_score_mask(genv.state[0, :genv.n_spins], genv.matrix)
+                    m = np.array(mask, dtype=np.float64)
+                    if not genv.reversible_spins:
+                        np.putmask(m, genv.state[0, :genv.n_spins] != -1, np.finfo(np.float64).min)
+                    a = int(m.argmax())
+                    if m[a] < 0:
+                        break
+                    _, _, gdone, _ = genv.step(a)
+                    gacts.append(a)
+                q = f"c{ci}_"
+                out[q + "target"] = np.array(target)
+                out[q + "mode"] = np.array(mode)
+                out[q + "J0"] = J0.astype(np.int8)
+                out[q + "J"] = J.astype(np.int8)
+                out[q + "T"] = np.int64(T)
+                out[q + "spins"] = spins.astype(np.int8)
+                out[q + "actions"] = np.asarray(actions, dtype=np.int32)
+                out[q + "obs"] = np.stack(rec["obs"])
+                for k in ("rew", "score", "nscore", "best_score", "best_nscore", "best_solution"):
+                    out[q + k] = np.asarray(rec[k], dtype=np.float64)
+                out[q + "done"] = np.asarray(rec["done"], dtype=bool)
+                out[q + "norms"] = np.asarray(norms, dtype=np.float64)   # mlr, qn, invalidity normaliser, lb
+                out[q + "greedy_actions"] = np.asarray(gacts, dtype=np.int32)
+                out[q + "greedy_best_solution"] = np.float64(genv.best_solution)
+                out[q + "greedy_best_score"] = np.float64(genv.best_score)
+                ci += 1
+    out["n_cases"] = np.int64(ci)
+    np.savez_compressed(os.path.join(HERE, "env_problems.npz"), **out)
+
+
 if __name__ == "__main__":
     random.seed(0)
     np.random.seed(0)
-    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "greedy_rollout", "greedy_solver"]
+    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "greedy_rollout", "greedy_solver",
+                              "env_problems"]
     for w in which:
         globals()["make_" + w]()
     for f in sorted(os.listdir(HERE)):

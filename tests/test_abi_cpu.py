@@ -55,3 +55,35 @@ def test_header_enums_match_reference_values():
         assert re.search(rf"ECO_OBS_{o.name}\s*=\s*{o.value}\b", src), o
     for r in u.RewardSignal:
         assert re.search(rf"ECO_REWARD_{r.name}\s*=\s*{r.value}\b", src), r
+
+
+def test_target_enums_and_config_validation():
+    """OptimisationTarget values, and the C-side config check (eco_env_state_bytes returns 0 for a config
+    eco_env_reset would reject): every set problem takes all 13 MAIN_OBSERVABLES; the cut scorers reject
+    the validity-mask observables (a TypeError in the reference); ENERGY has no scorer."""
+    import pytest
+    from eco_hip import _lib
+    from eco_hip.envs import utils as u
+    from eco_hip.envs.batched import make_config
+    src = open(os.path.join(REPO, "include", "eco_hip.h")).read()
+    for t in u.OptimisationTarget:
+        assert re.search(rf"ECO_TARGET_{t.name}\s*=\s*{t.value}\b", src), t
+    kw = dict(reward_signal=u.RewardSignal.BLS, extra_action=u.ExtraAction.NONE, norm_rewards=True,
+              basin_reward=1 / 20)
+    for t in (u.OptimisationTarget.MIN_COVER, u.OptimisationTarget.MAX_IND_SET, u.OptimisationTarget.MAX_CLIQUE,
+              u.OptimisationTarget.MIN_DOM_SET):
+        cfg = make_config(20, 40, observables=u.MAIN_OBSERVABLES, optimisation_target=t, **kw)
+        assert cfg.n_obs == 13 and _lib.obs_x_stride(cfg.n_obs) == 16
+        assert _lib.lib.eco_env_state_bytes(ctypes.byref(cfg), 4) > 0, t
+    for t in (u.OptimisationTarget.CUT, u.OptimisationTarget.MIN_CUT):
+        with pytest.raises(TypeError):
+            make_config(20, 40, observables=u.MAIN_OBSERVABLES, optimisation_target=t, **kw)
+        cfg = make_config(20, 40, observables=u.DEFAULT_OBSERVABLES, optimisation_target=t, **kw)
+        assert _lib.lib.eco_env_state_bytes(ctypes.byref(cfg), 4) > 0
+        cfg.n_obs = 13                                   # bypass the Python check: the library rejects it too
+        for i, o in enumerate(u.MAIN_OBSERVABLES):
+            cfg.obs_ids[i] = o.value
+        assert _lib.lib.eco_env_state_bytes(ctypes.byref(cfg), 4) == 0
+    cfg = make_config(20, 40, optimisation_target=u.OptimisationTarget.MIN_COVER, **kw)
+    cfg.optimisation_target = u.OptimisationTarget.ENERGY.value
+    assert _lib.lib.eco_env_state_bytes(ctypes.byref(cfg), 4) == 0
