@@ -42,7 +42,10 @@ constexpr int BF_FWD_END = BF_LAYER + 3 * BF_LAYER_STRIDE;
 constexpr int BFT_WF = BF_FWD_END;                   // Wf^T: 1 half
 constexpr int BFT_LAYER = BFT_WF + BF_HALF;          // + l * BF_LAYER_STRIDE: Wm^T (2 halves), then Wu^T
 constexpr int BF_TOTAL = BFT_LAYER + 3 * BF_LAYER_STRIDE;  // bf16 elements
-constexpr int PK_TOTAL = PK_BF + BF_TOTAL / 2;
+// node-feature columns 8..15 (n_obs_in > 8, MAIN_OBSERVABLES): W0 [64][8] and Wx [64][8] (row 63 zero)
+constexpr int PK_W0H = (PK_BF + BF_TOTAL / 2 + 3) & ~3;
+constexpr int PK_WXH = PK_W0H + 512;
+constexpr int PK_TOTAL = PK_WXH + 512;
 
 // k' -> input feature of the bf16 Linear operands: within each 64-feature block, k' = 32kc + 8q + j
 // (kc = 0,1; q = lane >> 4; j = 0..7) holds feature 16(2kc + (j >> 2)) + 4q + (j & 3), i.e. the two

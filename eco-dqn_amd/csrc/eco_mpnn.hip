@@ -48,7 +48,13 @@ __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __rest
   if (i >= PK_TOTAL) return;
   const FlatOffsets o = flat_offsets(nobs);
   float v = 0.f;
-  if (i < PK_WX) {
+  if (i >= PK_W0H) {  // feature columns 8..15
+    const bool wx = i >= PK_WXH;
+    const int j = i - (wx ? PK_WXH : PK_W0H);
+    const int r = j >> 3, c = 8 + (j & 7);
+    if (!wx) v = c < nobs ? f[o.W0 + r * nobs + c] : 0.f;
+    else v = (r < 63 && c < nobs) ? f[o.We + r * (1 + nobs) + 1 + c] : 0.f;
+  } else if (i < PK_WX) {
     const int r = i >> 3, c = i & 7;
     v = c < nobs ? f[o.W0 + r * nobs + c] : 0.f;
   } else if (i < PK_WA) {
@@ -145,8 +151,9 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
   const int c16 = lane & 15;
   const uint32_t* __restrict__ edges = a.gs.edges;
 
-  // ---- staging: x rows (WLDS), row info, Wf ----
-  if constexpr (WLDS) {
+  // ---- staging: x rows (WLDS, 8-float rows), row info, Wf ----
+  const bool xwide = a.xw == 16;  // features 8..15 (read from global memory, never staged)
+  if (WLDS && !xwide) {
     for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
       const int r = i >> 1;
       float4 v = zero4();
@@ -154,15 +161,22 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       st4(Xs + 8 * r + 4 * (i & 1), v);
     }
   }
-  // node features of row r (zero for padding rows)
+  // node features 0..7 of row r (zero for padding rows)
   auto xrow = [&](int r, float4& x0, float4& x1) {
-    if constexpr (WLDS) {
+    if (WLDS && !xwide) {
       x0 = f4(Xs + 8 * r);
       x1 = f4(Xs + 8 * r + 4);
     } else {
-      x0 = r < rows_valid ? f4(a.x + (R0 + r) * 8) : zero4();
-      x1 = r < rows_valid ? f4(a.x + (R0 + r) * 8 + 4) : zero4();
+      x0 = r < rows_valid ? f4(a.x + (R0 + r) * a.xw) : zero4();
+      x1 = r < rows_valid ? f4(a.x + (R0 + r) * a.xw + 4) : zero4();
     }
+  };
+  // w . x over features 8..15 (wide rows only)
+  auto xdot_hi = [&](int r, const float* wh) {
+    if (!xwide || r >= rows_valid) return 0.f;
+    const float4 x2 = f4(a.x + (R0 + r) * 16 + 8), x3 = f4(a.x + (R0 + r) * 16 + 12);
+    return wh[0] * x2.x + wh[1] * x2.y + wh[2] * x2.z + wh[3] * x2.w + wh[4] * x3.x + wh[5] * x3.y + wh[6] * x3.z +
+           wh[7] * x3.w;
   };
   for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
   for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
@@ -183,7 +197,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       float4 x0, x1;
       xrow(r, x0, x1);
       Hs[r * LDH + lane] = wx[0] * x0.x + wx[1] * x0.y + wx[2] * x0.z + wx[3] * x0.w + wx[4] * x1.x +
-                           wx[5] * x1.y + wx[6] * x1.z + wx[7] * x1.w;
+                           wx[5] * x1.y + wx[6] * x1.z + wx[7] * x1.w + xdot_hi(r, P + PK_WXH + lane * 8);
     }
   }
   __syncthreads();
@@ -261,7 +275,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_forward_kerne
       float4 x0, x1;
       xrow(r, x0, x1);
       const float z = relu(w0[0] * x0.x + w0[1] * x0.y + w0[2] * x0.z + w0[3] * x0.w + w0[4] * x1.x +
-                           w0[5] * x1.y + w0[6] * x1.z + w0[7] * x1.w);
+                           w0[5] * x1.y + w0[6] * x1.z + w0[7] * x1.w + xdot_hi(r, P + PK_W0H + lane * 8));
       if (SAVE && r < rows_valid) a.sv[(size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + lane] = z;
       Hs[r * LDH + lane] = z;
     }
@@ -425,7 +439,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
     RI[r] = pack_row_info(a, blk, r, rows_valid);
   }
   for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
-  if constexpr (WLDS) {
+  const bool xwide = a.xw == 16;  // features 8..15: read from global memory
+  if (WLDS && !xwide) {
     for (int i = threadIdx.x; i < rows_pad * 2; i += NT) {
       const int r = i >> 1;
       st4(Xs + 8 * r + 4 * (i & 1), r < rows_valid ? f4(a.x + (R0 + r) * 8 + 4 * (i & 1)) : zero4());
@@ -658,11 +673,12 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
         const bool valid = r < rows_valid;
         const RowInfo ri = row_info(RI, r);
         // z = Wx.x of the lane's node for its 16 features (same expression as forward phase A)
-        float4 x0 = zero4(), x1 = zero4();
+        float4 x0 = zero4(), x1 = zero4(), x2 = zero4(), x3 = zero4();
         if (valid) {
-          const float* xr = WLDS ? Xs + 8 * r : a.x + (R0 + r) * 8;
+          const float* xr = (WLDS && !xwide) ? Xs + 8 * r : a.x + (R0 + r) * a.xw;
           x0 = f4(xr);
           x1 = f4(xr + 4);
+          if (xwide) { x2 = f4(xr + 8); x3 = f4(xr + 12); }
         }
         float z[16], dz[16];
 #pragma unroll
@@ -673,6 +689,12 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 ? 2 : 1)) void mpnn_backward_kern
             const float4 w0 = f4(wx), w1 = f4(wx + 4);
             z[4 * c + i] = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
                            w1.z * x1.z + w1.w * x1.w;
+            if (xwide) {  // same left-to-right order as the forward's xdot_hi term
+              const float* wh = P + PK_WXH + (16 * c + 4 * s4 + i) * 8;
+              const float4 h0 = f4(wh), h1 = f4(wh + 4);
+              z[4 * c + i] += h0.x * x2.x + h0.y * x2.y + h0.z * x2.z + h0.w * x2.w + h1.x * x3.x + h1.y * x3.y +
+                              h1.z * x3.z + h1.w * x3.w;
+            }
           }
 #pragma unroll
         for (int i = 0; i < 16; ++i) dz[i] = 0.f;
@@ -908,7 +930,7 @@ __global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, 
 static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
                    const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope) {
   if (!packed || !gs || !graph_ids || !obs_x) return fail(ECO_ERR_ARG, "null argument");
-  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
+  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 16]");
   if (batch < 1) return fail(ECO_ERR_ARG, "batch must be >= 1");
   const int N = gs->n_spins;
   if (N < 1 || N > MPNN_MAX_SPINS_LARGE) return fail(ECO_ERR_ARG, "mpnn supports 1 <= N <= 2048");
@@ -916,7 +938,9 @@ static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco
     return fail(ECO_ERR_ARG, "bad norm_scope");
   a = MpnnArgs{};
   a.P = packed; a.gs = *gs; a.gids = graph_ids; a.B = batch; a.N = N; a.gpb = graphs_per_block(N);
-  a.nobs = n_obs_in; a.x = obs_x; a.norm_scope = norm_scope;
+  a.nobs = n_obs_in; a.xw = ECO_OBS_X_STRIDE(n_obs_in); a.x = obs_x; a.norm_scope = norm_scope;
+  if (a.xw != 8 && N > MPNN_MAX_SPINS)
+    return fail(ECO_ERR_ARG, "more than 8 node features need N <= 512 (the N > 512 kernel takes 8-float rows)");
   a.err = err_word();
   return ECO_OK;
 }
@@ -941,7 +965,7 @@ extern "C" size_t eco_mpnn_packed_count(void) { return (size_t)PK_TOTAL; }
 
 extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packed, eco_stream_t stream) {
   if (!params || !packed) return fail(ECO_ERR_ARG, "null params/packed");
-  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 8]");
+  if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 16]");
   pack_kernel<<<(PK_TOTAL + 255) / 256, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   return check_launch("mpnn_pack");
 }
@@ -1028,7 +1052,8 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     if (hipMemsetAsync(cmax, 0, sizeof(int), st) != hipSuccess) return fail(ECO_ERR_HIP, "memset failed");
     call_maxdeg_kernel<<<min(256, (batch + 255) / 256), 256, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
-  if (dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_forward_dense_launch(a, saved != nullptr, st);
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE"))
+    return mpnn_forward_dense_launch(a, saved != nullptr, st);
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
     const int rows_pad = (N + 15) & ~15;
@@ -1080,7 +1105,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.sv = (float*)saved;
   a.dq = dq;
   a.gr = (float*)gradws;
-  if (dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dense_launch(a, st);
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dense_launch(a, st);
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");

@@ -10,7 +10,8 @@ struct MpnnArgs {
   eco_graph_set gs;
   const int32_t* gids;
   int B, N, gpb, nobs;
-  const float* x;        // [B*N][8]
+  int xw;                // floats per node row of x: 8, or 16 when nobs > 8
+  const float* x;        // [B*N][xw]
   int norm_scope;
   const int* call_maxdeg;
   float* q;              // [B*N] or null
@@ -251,7 +252,7 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
       float qv = -INFINITY;
       if (v < N) {
         qv = Qb[gl * N + v];
-        allowed = a.act.reversible || (a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value);
+        allowed = a.act.reversible || (a.x[(R0 + gl * N + v) * a.xw] == a.act.allowed_value);
       }
       n_allowed += __popcll(__ballot(allowed));
       if (allowed && (qv > bestq || (qv == bestq && v < besti))) { bestq = qv; besti = v; }
@@ -274,7 +275,7 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
         action = -1;  // k-th allowed vertex
         for (int v0 = 0; v0 < N && action < 0; v0 += 64) {
           const int v = v0 + lane;
-          const bool al = v < N && a.x[(R0 + gl * N + v) * 8] == a.act.allowed_value;
+          const bool al = v < N && a.x[(R0 + gl * N + v) * a.xw] == a.act.allowed_value;
           const uint64_t bal = __ballot(al);
           const int c = __popcll(bal);
           if (k < c) {

@@ -212,18 +212,20 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, int n,
 
 // ------------------------------------------------------------------ replay ----
 // ReplayBuffer (dqn/utils.py:28-83) as a device ring of compact transitions:
-// node features of s and s' ([N][8] fp32), graph id, action, reward, done.
+// node features of s and s' ([N][x_stride] fp32), graph id, action, reward, done.
+__device__ __forceinline__ int xstride(const eco_replay& rb) { return rb.x_stride == 16 ? 16 : 8; }
+
 __global__ void replay_push_kernel(eco_replay rb, int pos, int B, const float* xs, const float* xn,
                                    const int32_t* gids, const int32_t* actions, const double* rewards,
                                    const uint8_t* dones) {
   const int b = blockIdx.y;
   if (b >= B) return;
   const int slot = (int)(((long long)pos + b) % rb.capacity);
-  const int per = rb.n_spins * 8 / 4;  // float4s per state
-  const float4* s4 = reinterpret_cast<const float4*>(xs + (size_t)b * rb.n_spins * 8);
-  const float4* n4 = reinterpret_cast<const float4*>(xn + (size_t)b * rb.n_spins * 8);
-  float4* ds = reinterpret_cast<float4*>(rb.xs + (size_t)slot * rb.n_spins * 8);
-  float4* dn = reinterpret_cast<float4*>(rb.xn + (size_t)slot * rb.n_spins * 8);
+  const int per = rb.n_spins * xstride(rb) / 4;  // float4s per state
+  const float4* s4 = reinterpret_cast<const float4*>(xs + (size_t)b * rb.n_spins * xstride(rb));
+  const float4* n4 = reinterpret_cast<const float4*>(xn + (size_t)b * rb.n_spins * xstride(rb));
+  float4* ds = reinterpret_cast<float4*>(rb.xs + (size_t)slot * rb.n_spins * xstride(rb));
+  float4* dn = reinterpret_cast<float4*>(rb.xn + (size_t)slot * rb.n_spins * xstride(rb));
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per; i += gridDim.x * blockDim.x) {
     ds[i] = s4[i];
     dn[i] = n4[i];
@@ -262,11 +264,11 @@ __global__ void replay_sample_kernel(eco_replay rb, int size, int M, uint64_t ke
   uint32_t x = (uint32_t)m;
   do { x = feistel(x, half, key); } while (x >= (uint32_t)size);
   const int slot = (int)x;
-  const int per = rb.n_spins * 8 / 4;
-  const float4* s4 = reinterpret_cast<const float4*>(rb.xs + (size_t)slot * rb.n_spins * 8);
-  const float4* n4 = reinterpret_cast<const float4*>(rb.xn + (size_t)slot * rb.n_spins * 8);
-  float4* ds = reinterpret_cast<float4*>(xs + (size_t)m * rb.n_spins * 8);
-  float4* dn = reinterpret_cast<float4*>(xn + (size_t)m * rb.n_spins * 8);
+  const int per = rb.n_spins * xstride(rb) / 4;
+  const float4* s4 = reinterpret_cast<const float4*>(rb.xs + (size_t)slot * rb.n_spins * xstride(rb));
+  const float4* n4 = reinterpret_cast<const float4*>(rb.xn + (size_t)slot * rb.n_spins * xstride(rb));
+  float4* ds = reinterpret_cast<float4*>(xs + (size_t)m * rb.n_spins * xstride(rb));
+  float4* dn = reinterpret_cast<float4*>(xn + (size_t)m * rb.n_spins * xstride(rb));
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per; i += gridDim.x * blockDim.x) {
     ds[i] = s4[i];
     dn[i] = n4[i];
@@ -324,8 +326,9 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
                     128, 0};
   }
   J.j[n++] = WJob{GR(GR_DUE), SV(SV_EAGG), nullptr, 64, 64, 0, 0, R, 64, fo.Wf, 64, 0};
-  J.j[n++] = WJob{GR(GR_DU0), obs_x, nullptr, 8, n_obs_in, 0, 0, R, 64, fo.W0, n_obs_in, 0};
-  J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, 8, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
+  const int xw = ECO_OBS_X_STRIDE(n_obs_in);
+  J.j[n++] = WJob{GR(GR_DU0), obs_x, nullptr, xw, n_obs_in, 0, 0, R, 64, fo.W0, n_obs_in, 0};
+  J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, xw, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
   wgrad_kernel<<<dim3(WG_PER_JOB, n), 256, 0, st>>>(J, slabs);
@@ -370,6 +373,7 @@ extern "C" int eco_replay_push(const eco_replay* rb, int32_t pos, int32_t batch,
                                const int32_t* graph_ids, const int32_t* actions, const double* rewards,
                                const uint8_t* dones, eco_stream_t stream) {
   if (!rb || !xs || !xn || !graph_ids || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
+  if (rb->x_stride != 0 && rb->x_stride != 8 && rb->x_stride != 16) return fail(ECO_ERR_ARG, "x_stride must be 8 or 16");
   if (batch < 1 || rb->capacity < 1 || pos < 0) return fail(ECO_ERR_ARG, "bad batch/capacity/pos");
   replay_push_kernel<<<dim3(1, batch), 256, 0, (hipStream_t)stream>>>(*rb, pos, batch, xs, xn, graph_ids, actions,
                                                                       rewards, dones);
@@ -380,6 +384,7 @@ extern "C" int eco_replay_sample(const eco_replay* rb, int32_t size, int32_t m, 
                                  float* xs, float* xn, int32_t* graph_ids, int32_t* actions, float* rewards,
                                  float* dones, eco_stream_t stream) {
   if (!rb || !xs || !xn || !graph_ids || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
+  if (rb->x_stride != 0 && rb->x_stride != 8 && rb->x_stride != 16) return fail(ECO_ERR_ARG, "x_stride must be 8 or 16");
   if (size < m || m < 1 || size > rb->capacity)
     return fail(ECO_ERR_ARG, "replay sample: need m <= size <= capacity (random.sample without replacement)");
   replay_sample_kernel<<<dim3(1, m), 256, 0, (hipStream_t)stream>>>(*rb, size, m, rng3(seed, counter, 0x5A5A),

@@ -19,7 +19,7 @@ lib = ctypes.CDLL(LIB_PATH)
 ECO_OK, ECO_ERR_ARG, ECO_ERR_HIP, ECO_ERR_PAST_END, ECO_ERR_BASIS, ECO_ERR_TARGET, ECO_ERR_OBSERVABLE, \
     ECO_ERR_GRAPH = range(8)
 ECO_MAX_OBS = 16          # observables per env (MAIN_OBSERVABLES has 13)
-ECO_MPNN_MAX_OBS = 8      # MPNN n_obs_in limit (node-feature rows of 8 floats)
+ECO_MPNN_MAX_OBS = 16     # MPNN n_obs_in limit (node-feature rows of obs_x_stride(n_obs_in) floats)
 ECO_ENV_SCALARS = 16
 ECO_TARGET_CUT, ECO_TARGET_ENERGY, ECO_TARGET_MIN_COVER, ECO_TARGET_MIN_CUT, ECO_TARGET_MAX_IND_SET, \
     ECO_TARGET_MAX_CLIQUE, ECO_TARGET_MIN_DOM_SET = range(1, 8)
@@ -52,7 +52,8 @@ class GraphSet(ctypes.Structure):
 
 
 class Replay(ctypes.Structure):
-    _fields_ = [("capacity", ctypes.c_int32), ("n_spins", ctypes.c_int32), ("xs", ctypes.c_void_p),
+    _fields_ = [("capacity", ctypes.c_int32), ("n_spins", ctypes.c_int32), ("x_stride", ctypes.c_int32),
+                ("xs", ctypes.c_void_p),
                 ("xn", ctypes.c_void_p), ("gid", ctypes.c_void_p), ("act", ctypes.c_void_p),
                 ("rew", ctypes.c_void_p), ("done", ctypes.c_void_p)]
 

@@ -99,7 +99,8 @@ class DQN:
         self.B = envs.n_envs
         self.N = envs.n_spins
         self.M = int(train_minibatch or minibatch_size)
-        self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed)
+        self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed,
+                                          n_obs=envs.n_obs)
         self.replay_ratio = minibatch_size / float(update_frequency)
         # reference: one target sync per update_target_frequency env-steps = that many
         # env-steps' worth of replayed samples

@@ -39,18 +39,19 @@ def set_global_seed(seed, env=None):
 class ReplayBuffer:
     """Device ring of compact transitions (eco_replay, include/eco_hip.h)."""
 
-    def __init__(self, capacity, n_spins, device="cuda", seed=0):
+    def __init__(self, capacity, n_spins, device="cuda", seed=0, n_obs=7):
         self._capacity = int(capacity)
         self.n_spins = n_spins
+        self.x_stride = _lib.obs_x_stride(n_obs)
         dev = torch.device(device)
         self.device = dev
-        self.xs = torch.zeros(capacity, n_spins, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=dev)
-        self.xn = torch.zeros(capacity, n_spins, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=dev)
+        self.xs = torch.zeros(capacity, n_spins, self.x_stride, dtype=torch.float32, device=dev)
+        self.xn = torch.zeros(capacity, n_spins, self.x_stride, dtype=torch.float32, device=dev)
         self.gid = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.act = torch.zeros(capacity, dtype=torch.int32, device=dev)
         self.rew = torch.zeros(capacity, dtype=torch.float32, device=dev)
         self.done = torch.zeros(capacity, dtype=torch.float32, device=dev)
-        self.rb = _lib.Replay(self._capacity, n_spins, self.xs.data_ptr(), self.xn.data_ptr(), self.gid.data_ptr(),
+        self.rb = _lib.Replay(self._capacity, n_spins, self.x_stride, self.xs.data_ptr(), self.xn.data_ptr(), self.gid.data_ptr(),
                               self.act.data_ptr(), self.rew.data_ptr(), self.done.data_ptr())
         self._position = 0
         self._size = 0
@@ -70,8 +71,8 @@ class ReplayBuffer:
     def _buffers(self, m):
         if m not in self._out:
             dev = self.device
-            self._out[m] = (torch.empty(m, self.n_spins, _lib.ECO_MPNN_MAX_OBS, device=dev),
-                            torch.empty(m, self.n_spins, _lib.ECO_MPNN_MAX_OBS, device=dev),
+            self._out[m] = (torch.empty(m, self.n_spins, self.x_stride, device=dev),
+                            torch.empty(m, self.n_spins, self.x_stride, device=dev),
                             torch.empty(m, dtype=torch.int32, device=dev), torch.empty(m, dtype=torch.int32, device=dev),
                             torch.empty(m, device=dev), torch.empty(m, device=dev))
         return self._out[m]

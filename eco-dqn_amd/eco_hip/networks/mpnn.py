@@ -41,7 +41,7 @@ class MPNN(torch.nn.Module):
             raise NotImplementedError("eco_hip implements the ECO-DQN MPNN configuration used by the "
                                       "reference (n_layers=3, n_features=64, untied, no hidden readout)")
         if not 1 <= n_obs_in <= _lib.ECO_MPNN_MAX_OBS:
-            raise ValueError("n_obs_in must be in [1, 8]")
+            raise ValueError("n_obs_in must be in [1, 16]")
         self.n_obs_in = n_obs_in
         self.n_layers = n_layers
         self.n_features = n_features
@@ -103,6 +103,11 @@ class MPNN(torch.nn.Module):
                     p.copy_((torch.rand(p.shape, generator=generator) * 2 - 1) * bound)
         self._packed_version = -1
 
+    def _check_x(self, obs_x):
+        w = _lib.obs_x_stride(self.n_obs_in)
+        if obs_x.dim() != 3 or obs_x.shape[2] != w or not obs_x.is_contiguous() or obs_x.dtype != torch.float32:
+            raise ValueError(f"obs_x must be a contiguous float32 [B, N, {w}] tensor for n_obs_in={self.n_obs_in}")
+
     def _workspace(self, n_spins, batch):
         need = _lib.lib.eco_mpnn_workspace_bytes(n_spins, batch)
         if self._ws is None or self._ws.numel() < need:
@@ -112,10 +117,11 @@ class MPNN(torch.nn.Module):
     # ---- fast path: graphs resident in a GraphStore ----
     def forward_graphs(self, obs_x, graphs, graph_ids, norm_scope=_lib.ECO_NORM_PER_GRAPH, q_out=None,
                        act=None, actions_out=None, saved=None, stream=None):
-        """Q [B, N] for node features obs_x [B, N, 8] on graphs graph_ids [B] of `graphs`.
+        """Q [B, N] for node features obs_x [B, N, W] (W = 8, or 16 for n_obs_in > 8) on graphs graph_ids [B].
         act: optional ActConfig -> fused epsilon-greedy actions written to actions_out [B] int32.
         saved: optional buffer (saved_bytes) that receives the activations for backward()."""
         B, N = obs_x.shape[0], obs_x.shape[1]
+        self._check_x(obs_x)
         self._ensure_packed(stream)
         if q_out is None and act is None:
             q_out = torch.empty(B, N, dtype=torch.float32, device=obs_x.device)
@@ -140,6 +146,7 @@ class MPNN(torch.nn.Module):
         """loss.backward(): grad_out[flat] = dLoss/dparams for dq = dLoss/dQ [B, N] of the forward that
         filled `saved` (forward_graphs(..., norm_scope=ECO_NORM_PER_CALL, saved=...))."""
         B, N = obs_x.shape[0], obs_x.shape[1]
+        self._check_x(obs_x)
         need = _lib.lib.eco_mpnn_backward_workspace_bytes(N, B)
         if workspace is None or workspace.numel() < need:
             workspace = torch.empty(need, dtype=torch.uint8, device=obs_x.device)
@@ -168,7 +175,7 @@ class MPNN(torch.nn.Module):
             view = obs
         B, R, N = view.shape
         k = self.n_obs_in
-        x = torch.zeros(B, N, _lib.ECO_MPNN_MAX_OBS, dtype=torch.float32, device=self.flat.device)
+        x = torch.zeros(B, N, _lib.obs_x_stride(k), dtype=torch.float32, device=self.flat.device)
         x[:, :, :k] = view[:, :k, :].transpose(1, 2).to(x.device, torch.float32)
         adj = view[:, k:, :].detach().cpu().numpy()
         store = GraphStore(*dense_to_csr([a.T for a in adj]), device=self.flat.device)

@@ -59,7 +59,7 @@ enum { ECO_TARGET_CUT = 1, ECO_TARGET_ENERGY = 2, ECO_TARGET_MIN_COVER = 3, ECO_
        ECO_TARGET_MAX_IND_SET = 5, ECO_TARGET_MAX_CLIQUE = 6, ECO_TARGET_MIN_DOM_SET = 7 };
 
 #define ECO_MAX_OBS 16     /* observables per env (all 13 of MAIN_OBSERVABLES, src/envs/utils.py:76-88) */
-#define ECO_MPNN_MAX_OBS 8 /* MPNN n_obs_in limit (its node-feature rows are 8 floats) */
+#define ECO_MPNN_MAX_OBS 16 /* MPNN n_obs_in limit; node-feature rows are ECO_OBS_X_STRIDE(n_obs_in) floats */
 /* obs_x row width in floats for n_obs observables: 8 up to 8 observables, else 16 */
 #define ECO_OBS_X_STRIDE(n_obs) ((n_obs) <= 8 ? 8 : 16)
 #define ECO_MAX_SPINS 2048 /* largest N the env kernels take (wave-per-episode, 32 vertices per lane) */
@@ -207,7 +207,9 @@ size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch);
 size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch);
 
 /* MPNN.forward (mpnn.py:40-77) on B graphs at once.
- * obs_x[B][N][8]: node features; adjacency = graphs graph_ids[B] of `gs`.
+ * obs_x[B][N][ECO_OBS_X_STRIDE(n_obs_in)]: node features; adjacency = graphs graph_ids[B] of `gs`.
+ * Up to 8 features every kernel applies; 9..16 features (MAIN_OBSERVABLES) run the CSR-gather kernels
+ * for N <= 512 (the dense-aggregation and N > 512 kernels take 8-float rows).
  * q[B][N] fp32 (may be NULL when only actions are wanted).
  * act / actions[B]: optional fused epsilon-greedy action selection.
  * saved: NULL for inference; for the training forward of train_step (dqn.py:437)
@@ -242,11 +244,12 @@ int eco_adam(float *params, const float *grad, float *exp_avg, float *exp_avg_sq
              eco_stream_t stream);
 
 /* ReplayBuffer (dqn/utils.py:28-83) as a device ring of compact transitions.  Buffers are
- * caller-owned: xs/xn [capacity][N][8] fp32 node features of s and s'; graph id, action,
+ * caller-owned: xs/xn [capacity][N][x_stride] fp32 node features of s and s'; graph id, action,
  * reward (fp32, dqn.py:299), done (fp32). */
 typedef struct {
   int32_t capacity;
   int32_t n_spins;
+  int32_t x_stride;  /* floats per node row: ECO_OBS_X_STRIDE(n_obs) (8 or 16; 0 means 8) */
   float *xs;
   float *xn;
   int32_t *gid;
