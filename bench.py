@@ -33,6 +33,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak ~8 TB/s
 
 
 def mpnn_flops(nnz, n):
@@ -123,11 +124,15 @@ def main():
     ap.add_argument("--graph", default="ER", choices=["ER", "BA"],
                     help="training graphs: ER(n, p=--param) (configs[2]) or BA(n, m=--param) (configs[3])")
     ap.add_argument("--param", type=float, default=None, help="ER p (default 0.15) / BA m (default 4)")
-    ap.add_argument("--workload", default="train", choices=["train", "rollout", "gset", "er20"],
+    ap.add_argument("--workload", default="train", choices=["train", "rollout", "gset", "er20", "envstep"],
                     help="train = configs[2] (default); rollout = its act + env step half; "
                          "gset = configs[4] per GPU: 1024 episodes of greedy best-cut search on one "
                          "G22-like ER(2000, p=0.01) unit-weight graph; er20 = configs[1]: 4096 ER-20 "
-                         "episodes, MPNN forward + greedy act + env step")
+                         "episodes, MPNN forward + greedy act + env step; envstep = the env step kernel "
+                         "alone (SURVEY.md 8d sub-bench) for --target")
+    ap.add_argument("--target", default="CUT",
+                    choices=["CUT", "MIN_COVER", "MIN_CUT", "MAX_IND_SET", "MAX_CLIQUE", "MIN_DOM_SET"],
+                    help="envstep: OptimisationTarget (set problems use MAIN_OBSERVABLES and unit weights)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -143,6 +148,8 @@ def main():
 
     if args.workload in ("gset", "er20"):
         return inference_bench(args, world, rank, dev, dist)
+    if args.workload == "envstep":
+        return envstep_bench(args, world, rank, dev, dist)
 
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
@@ -332,6 +339,74 @@ def inference_bench(args, world, rank, dev, dist):
                          "frac": fl / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                          "avg_launch_ms": fwd_ms, "flops_per_launch": fl},
             "best_cut_after_steps": best_cut,
+        }
+        print(json.dumps(out))
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+def envstep_bench(args, world, rank, dev, dist):
+    """SURVEY.md 8d sub-bench: the batched env step kernel alone (spinsystem.py:355-559 for the chosen
+    scorer), random actions drawn beforehand, B episodes of ER(n, 0.15).  HBM-bound: algorithmic bytes per
+    env-step = state read + write (spins 1, neighbour sum 4, time-since-flip 2 B per vertex, best spins read)
+    + fp32 feature rows written (4 W B per vertex) + the flipped vertex's CSR row (+ every row for
+    MinDomSet's neighbour counts)."""
+    from eco_hip import _lib
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, MAIN_OBSERVABLES, RewardSignal, ExtraAction,
+                                    OptimisationTarget)
+    from eco_hip.parallel import max_over_ranks
+    B, n = args.envs, args.n
+    T = 2 * n
+    cut_like = args.target in ("CUT", "MIN_CUT")
+    obs = DEFAULT_OBSERVABLES if cut_like else MAIN_OBSERVABLES
+    store = GraphStore.random("ER", B, n, 0.15, seed=1234 + rank, weights="discrete" if cut_like else "uniform",
+                              device=dev)
+    env = VecSpinSystem(store, B, T, observables=obs, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget[args.target],
+                        norm_rewards=True, basin_reward=1. / n)
+    env.reset(graph_ids=np.arange(B), seed=1234 + rank)
+    g = torch.Generator(device=dev).manual_seed(7 + rank)
+    steps = min(args.steps, T - args.warmup)
+    acts = torch.randint(0, n, (args.warmup + steps, B), generator=g, device=dev, dtype=torch.int32)
+    for i in range(args.warmup):
+        env.step(acts[i])
+    env.check_errors()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        env.step(acts[args.warmup + i])
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = max_over_ranks(time.perf_counter() - t0, device=dev)
+    env.check_errors()
+    k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    nnz = float(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
+    W = _lib.obs_x_stride(len(obs))
+    per_step = B * (n * (2 * (1 + 4 + 2) + 1 + 4 * W) + 4 * nnz / n + 2 * 192 +
+                    (4 * nnz if args.target == "MIN_DOM_SET" else 0))
+    achieved = per_step / (k_ms * 1e-3) / 1e9
+    if rank == 0:
+        out = {
+            "metric": f"env-steps/sec (batched episodes) on ER-{n} {args.target}: env step kernel only",
+            "value": B * steps * world / dt, "unit": "env-steps/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64+int (env)",
+            "data": f"synthetic: seeded ER({n}, 0.15) graphs, one per episode; uniform random actions",
+            "config": {"workload": f"ER_{n}spin x{B} episodes/GPU: env step only ({args.target}, "
+                                   f"{len(obs)} observables)", "n_spins": n, "envs_per_gpu": B, "max_steps": T,
+                       "parallelism": f"episodes sharded, dp{world}, no collective"},
+            "roofline": {"bound": "hbm", "kernel": "env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "avg_launch_ms": k_ms, "bytes_per_launch": per_step},
         }
         print(json.dumps(out))
     if dist:

@@ -177,6 +177,34 @@ __device__ __forceinline__ void mm_bf3(f32x4 (&acc)[4], const float4 (&x)[4], co
   }
 }
 
+// mm_bf3 with the fragment loads of one output tile at a time in flight (weights streamed from L2 by the
+// CSR-gather kernels, where the register budget, not the load latency, is the constraint)
+__device__ __forceinline__ void mm_bf3_lean(f32x4 (&acc)[4], const float4 (&x)[4], const uint16_t* WH, int lane) {
+  // opaque to the optimiser: the same fragments are NOT hoisted/CSE'd across the calls of consecutive
+  // tiles (which would keep 24 fragments = 96 VGPRs live per Linear half)
+  uint64_t wp = (uint64_t)WH;
+  asm volatile("" : "+s"(wp));
+  const uint16_t* wl = reinterpret_cast<const uint16_t*>(wp) + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    bf16x8 x1, x2, x3;
+    split_frag(x[2 * kc2], x[2 * kc2 + 1], x1, x2, x3);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      const bf16x8 w3 = *reinterpret_cast<const bf16x8*>(wl + ((2 * 4 + nt) * 2 + kc2) * BF_FRAG);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3, x1, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x2, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x3, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x1, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x2, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, acc[nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 // Two output halves (fragment sets WH0, WH1) of one 64-input transposed Linear, sharing the split of x.
 __device__ __forceinline__ void mm_bf3x2(f32x4 (&acc0)[4], f32x4 (&acc1)[4], const float4 (&x)[4],
                                          const uint16_t* WH0, const uint16_t* WH1, int lane) {

@@ -32,7 +32,8 @@ def _flat_to_dict(flat):
     return out
 
 
-@pytest.mark.parametrize("kind,n,B,param", [("ER", 20, 64, 0.15), ("ER", 200, 12, 0.15), ("BA", 60, 20, 4)])
+@pytest.mark.parametrize("kind,n,B,param", [("ER", 20, 64, 0.15), ("ER", 200, 12, 0.15), ("BA", 60, 20, 4),
+                                          ("BA", 300, 6, 4), ("BA", 500, 4, 4)])
 def test_backward_matches_autograd(kind, n, B, param):
     from eco_hip.graphs import GraphStore
     from eco_hip.networks.mpnn import MPNN
