@@ -397,6 +397,17 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
 }
 
 // ============================================================== backward ====
+// y[0..127] += W^T x for one 64-input transposed Linear from its two bf16x3 output-half fragment sets
+__device__ __forceinline__ void bf3_t2(f32x4 (&d8)[8], const float4 (&x)[4], const uint16_t* WT, int lane) {
+  f32x4 lo[4], hi[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) { lo[nt] = d8[nt]; hi[nt] = d8[4 + nt]; }
+  mm_bf3_lean(lo, x, WT, lane);
+  mm_bf3_lean(hi, x, WT + BF_HALF, lane);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) { d8[nt] = lo[nt]; d8[4 + nt] = hi[nt]; }
+}
+
 // Gradient of loss w.r.t. all MPNN parameters given dq = dLoss/dQ [B][N], for the
 // forward saved in a.sv.  This kernel produces the activation gradients (the
 // pre-activation gradients dY of every Linear, stored [R][64]) and the small
@@ -531,9 +542,12 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
   // Every Linear runs with the weight as the MFMA A operand (mm_k<.., true>): outputs arrive in the
   // node-operand layout (lane: node l&15, features 16c + 4(l>>4) + i), so the chain
   // duu -> [dh_direct, dm] -> dum -> [dagg, de] needs no transpose and rows are stored as float4.
+  const uint16_t* BFP = reinterpret_cast<const uint16_t*>(P + PK_BF);
   for (int layer = 2; layer >= 0; --layer) {
     const float* WmT = P + PK_LAYERT + layer * 16384;  // [128][64]
     const float* WuT = WmT + 8192;                      // [128][64]
+    // weights from L2 (no LDS staging): bf16x3-split transposed fragments, [out half][p][nt][kc2]
+    const uint16_t* BFT = BFP + BFT_LAYER + layer * BF_LAYER_STRIDE;  // Wm^T halves, then Wu^T halves
     if constexpr (WLDS) {  // previous readers of Wl finished at the last barrier
       stage_rows<NT>(Wl, LDH, WuT, 64, 128, 64);
       stage_rows<NT>(Wl + 128 * LDH, LDH, WmT, 64, 128, 64);
@@ -562,7 +576,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (WLDS) mm_k<8, 4, true>(d8, duu, Wl, LDH, lane);
-        else mm_k<8, 4, true>(d8, duu, WuT, 64, lane);
+        else bf3_t2(d8, duu, BFT + 2 * BF_HALF, lane);
         // dum = dm * [m > 0]
         float4 dum[4];
 #pragma unroll
@@ -578,7 +592,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) d8[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (WLDS) mm_k<8, 4, true>(d8, dum, Wl + 128 * LDH, LDH, lane);
-        else mm_k<8, 4, true>(d8, dum, WmT, 64, lane);
+        else bf3_t2(d8, dum, BFT, lane);
         const float nf = (float)row_info(RI, r).norm;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -656,7 +670,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d4[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (WLDS) mm_k<4, 4, true>(d4, due, Wl, LDH, lane);
-      else mm_k<4, 4, true>(d4, due, P + PK_WFT, 64, lane);
+      else mm_bf3_lean(d4, due, reinterpret_cast<const uint16_t*>(P + PK_BF) + BFT_WF, lane);
       const float nf = (float)row_info(RI, r).norm;
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -1035,10 +1049,10 @@ static KCfg pick_cfg(int N, int gpb, bool backward) {
   }
   // weights from L2, 8 waves (2 per SIMD: the block owns the CU through its LDS) when 4 tiles per
   // wave suffice; measured at BA-500: forward 15 % faster than 4 waves x 8 tiles, backward slower
-  if (!backward && (!force_nw || force_nw == 8)) {
+  if (!force_nw || force_nw == 8) {
     c.nw = 8;
     c.wlds = false;
-    c.lds = lds_bytes(rows_pad, gpb, 8, false, false);
+    c.lds = lds_bytes(rows_pad, gpb, 8, false, backward);
     c.maxt = (ntiles + 7) / 8;
     if (c.lds <= LDS_MAX && c.maxt <= 4) return c;
   }
@@ -1139,6 +1153,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   if (k.wlds && k.nw == 8 && k.maxt <= 2) ECO_LAUNCH_BWD(2, 8, true);
   else if (k.wlds && k.nw == 8) ECO_LAUNCH_BWD(4, 8, true);
   else if (k.wlds && k.maxt <= 4) ECO_LAUNCH_BWD(4, 4, true);
+  else if (k.nw == 8 && k.maxt <= 4) ECO_LAUNCH_BWD(4, 8, false);
   else if (k.maxt <= 4) ECO_LAUNCH_BWD(4, 4, false);
   else if (k.maxt <= 8) ECO_LAUNCH_BWD(8, 4, false);
   else return fail(ECO_ERR_ARG, "graph block too large");

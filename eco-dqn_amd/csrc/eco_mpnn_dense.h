@@ -182,9 +182,10 @@ __device__ __forceinline__ void mm_bf3(f32x4 (&acc)[4], const float4 (&x)[4], co
 __device__ __forceinline__ void mm_bf3_lean(f32x4 (&acc)[4], const float4 (&x)[4], const uint16_t* WH, int lane) {
   // opaque to the optimiser: the same fragments are NOT hoisted/CSE'd across the calls of consecutive
   // tiles (which would keep 24 fragments = 96 VGPRs live per Linear half)
-  uint64_t wp = (uint64_t)WH;
-  asm volatile("" : "+s"(wp));
-  const uint16_t* wl = reinterpret_cast<const uint16_t*>(wp) + lane * 8;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)WH);  // wave-uniform pointer
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)WH >> 32));
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  const uint16_t* wl = reinterpret_cast<const uint16_t*>(((uint64_t)hi << 32) | lo) + lane * 8;
 #pragma unroll
   for (int kc2 = 0; kc2 < 2; ++kc2) {
     bf16x8 x1, x2, x3;
