@@ -223,18 +223,20 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
 // SpinSystemBase.step (spinsystem.py:355-559), ExtraAction.NONE, memory_length None.
 template <int VPT>
 __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
+  extern __shared__ int32_t d_lds[];  // [4 waves][N] row deltas
   const int lane = threadIdx.x & 63;
-  const int e = uniform_i(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int wv = threadIdx.x >> 6;
+  const int e = uniform_i(blockIdx.x * 4 + wv);
   if (e >= a.B) return;
   const int N = a.cfg.n_spins;
   const int T = a.cfg.max_steps;
   const EnvLayout& L = a.L;
   EpScal* sc = scal_ptr(a) + e;
+  const int act = uniform_i(a.actions[e]);  // loaded alongside the done flag
   if (sc->done) {  // auto-masked
     if (lane == 0) { a.rewards[e] = 0.0; a.dones[e] = 1; }
     return;
   }
-  const int act = uniform_i(a.actions[e]);
   if (act < 0 || act >= N) {
     if (lane == 0) { atomicCAS(a.err, 0, ECO_ERR_ARG); a.rewards[e] = 0.0; a.dones[e] = 0; }
     return;
@@ -244,12 +246,10 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   int32_t* gh = (int32_t*)(a.state + L.off_field) + (size_t)e * N;
   int16_t* gt = (int16_t*)(a.state + L.off_tsf) + (size_t)e * N;
   int8_t* gb = (int8_t*)(a.state + L.off_best) + (size_t)e * N;
-  const int sa_old = gsp[act];
-  const double qn = sc->qn, mlr = sc->mlr;
-  const double delta = (double)sa_old * (double)gh[act];  // f64 product: keeps -0.0 like the reference
-  const double delta_n = delta / qn;     // get_normalized_score_mask(state)[action] (:394)
-  const double score = sc->score + delta;           // :399
-  const double nscore = sc->nscore + delta_n;       // :400 (accumulated)
+  const int gid = sc->graph;
+  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
+  const uint32_t* ed = a.gs.edges + a.gs.edge_base[gid];
+  const int q0 = rp[act], q1 = rp[act + 1];
   int s[VPT], h[VPT], tsf[VPT], bs[VPT], g[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
@@ -257,23 +257,15 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
     if (v < N) { s[k] = gsp[v]; h[k] = gh[v]; tsf[k] = gt[v]; bs[k] = gb[v]; }
     else { s[k] = 0; h[k] = 0; tsf[k] = 0; bs[k] = 0; }
   }
+  int sa_old, ha;
+  read_vertex<VPT>(s, h, act, sa_old, ha);
+  const double qn = sc->qn, mlr = sc->mlr;
+  const double delta = (double)sa_old * (double)ha;  // f64 product: keeps -0.0 like the reference
+  const double delta_n = delta / qn;     // get_normalized_score_mask(state)[action] (:394)
+  const double score = sc->score + delta;           // :399
+  const double nscore = sc->nscore + delta_n;       // :400 (accumulated)
   // incremental local field: h_j -= 2 w_aj s_a(old) over the CSR row of `act`
-  {
-    const int gid = sc->graph;
-    const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
-    const uint32_t* ed = a.gs.edges + a.gs.edge_base[gid];
-    const int q1 = rp[act + 1];
-    for (int q = rp[act]; q < q1; ++q) {
-      const uint32_t x = ed[q];
-      const int j = edge_col(x);
-      const int d = -2 * edge_w(x) * sa_old;
-      if ((j & 63) == lane) {
-        const int kk = j >> 6;
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) h[k] += (k == kk) ? d : 0;
-      }
-    }
-  }
+  row_update<VPT>(d_lds + wv * N, ed, q0, q1, N, lane, h, [&](int w) { return -2 * w * sa_old; });
   // flip + time-since-flip counters (:397, :492-497)
   int cnt = 0;
   uint64_t words[VPT];
@@ -566,8 +558,8 @@ extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, 
   a.actions = actions; a.rewards = rewards; a.dones = dones; a.obs_x = obs_x; a.obs_f64 = obs_f64;
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (batch + 3) / 4;
-  if (generic_target(cfg)) return env_step_problem_launch(a, blocks, (size_t)4 * cfg->n_spins, st);
-  ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, 0, st>>>(a)));
+  if (generic_target(cfg)) return env_step_problem_launch(a, blocks, env_step_lds(cfg->n_spins), st);
+  ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, (size_t)16 * cfg->n_spins, st>>>(a)));
   return check_launch("env_step");
 }
 

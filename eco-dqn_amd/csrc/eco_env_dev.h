@@ -46,6 +46,41 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Pre-flip spin and field of vertex `act` (lane act & 63, slot act >> 6) from the wave's registers.
+template <int VPT>
+__device__ __forceinline__ void read_vertex(const int (&s)[VPT], const int (&f)[VPT], int act, int& sa, int& fa) {
+  const int kk = act >> 6, la = act & 63;
+  sa = 0;
+  fa = 0;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k)
+    if (k == kk) { sa = __builtin_amdgcn_readlane(s[k], la); fa = __builtin_amdgcn_readlane(f[k], la); }
+}
+
+// f_j += coef(J_ja) for every neighbour j of `act`: the lanes load the CSR row in parallel and scatter the
+// deltas through the wave's LDS slice dl[N] (a row has distinct columns, so the stores never collide) --
+// one round of loads instead of deg(a) dependent ones.
+template <int VPT, class Coef>
+__device__ __forceinline__ void row_update(int32_t* dl, const uint32_t* ed, int q0, int q1, int N, int lane,
+                                           int (&f)[VPT], Coef coef) {
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) dl[v] = 0;
+  }
+  wave_lds_sync();
+  for (int q = q0 + lane; q < q1; q += 64) {
+    const uint32_t x = ed[q];
+    dl[edge_col(x)] = coef(edge_w(x));
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) f[k] += dl[v];
+  }
+}
+
 // HistoryBuffer.update (src/envs/utils.py:438-464): is the flipped-vertex set after flipping `act` new?
 // The set is identified by the spin configuration (words = ballot(s > 0) per 64 vertices); a Zobrist
 // hash of the set indexes an open-addressing table of the episode's visited configurations.  The
@@ -65,8 +100,9 @@ __device__ __forceinline__ bool history_update(const EnvArgs& a, int e, int lane
   int slot = (int)(hash & (uint64_t)(cap - 1));
   for (;;) {
     const uint32_t id = vidx[slot];
+    const uint64_t hs = vh[slot];  // issued together with the index load
     if (id == 0u) break;
-    if (vh[slot] == hash) {
+    if (hs == hash) {
       bool same = true;
 #pragma unroll
       for (int k = 0; k < VPT; ++k) same = same && (k >= W || vst[(size_t)(id - 1) * W + k] == words[k]);
@@ -90,6 +126,9 @@ __device__ __forceinline__ bool history_update(const EnvArgs& a, int e, int lane
 }
 
 // vertices per lane for N spins (one 64-lane wave per episode)
+// dynamic LDS of the step kernels: int32 row deltas [4 waves][N], then MinDomSet codes [4][N]
+inline size_t env_step_lds(int N) { return (size_t)4 * N * 4 + (size_t)4 * N; }
+
 #define ECO_DISPATCH_VPT(N, CALL)                                   \
   do {                                                              \
     if ((N) <= 64) { constexpr int V = 1; CALL; }                   \
@@ -100,7 +139,7 @@ __device__ __forceinline__ bool history_update(const EnvArgs& a, int e, int lane
     else { constexpr int V = 32; CALL; }                            \
   } while (0)
 
-// generic-scorer launches (eco_env_problems.hip): 4 episodes per 256-thread block, lds = 4 N bytes
+// generic-scorer launches (eco_env_problems.hip): 4 episodes per 256-thread block, lds = env_step_lds(N)
 int env_reset_problem_launch(const EnvArgs& a, int blocks, size_t lds, hipStream_t st);
 int env_step_problem_launch(const EnvArgs& a, int blocks, size_t lds, hipStream_t st);
 int env_greedy_problem_launch(const EnvArgs& a, int32_t* actions, int blocks, size_t lds, hipStream_t st);

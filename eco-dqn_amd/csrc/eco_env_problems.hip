@@ -350,7 +350,7 @@ __device__ __forceinline__ FlipDelta flip_delta(int tgt, int sa, int Fa, int n1,
 // SpinSystemBase.step (spinsystem.py:355-559) for the generic scorers.
 template <int VPT>
 __global__ __launch_bounds__(256) void env_step_problem_kernel(EnvArgs a) {
-  extern __shared__ uint8_t c_lds[];  // [4 waves][N] MinDomSet codes
+  extern __shared__ int32_t d_lds[];  // [4 waves][N] row deltas, then [4 waves][N] MinDomSet codes
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int e = uniform_i(blockIdx.x * 4 + wv);
@@ -360,12 +360,13 @@ __global__ __launch_bounds__(256) void env_step_problem_kernel(EnvArgs a) {
   const int tgt = a.cfg.optimisation_target;
   const bool cut_like = tgt == ECO_TARGET_MIN_CUT;
   const EnvLayout& L = a.L;
+  uint8_t* c_lds = reinterpret_cast<uint8_t*>(d_lds + 4 * N);
   EpScal* sc = scal_ptr(a) + e;
+  const int act = uniform_i(a.actions[e]);  // loaded alongside the done flag
   if (sc->done) {
     if (lane == 0) { a.rewards[e] = 0.0; a.dones[e] = 1; }
     return;
   }
-  const int act = uniform_i(a.actions[e]);
   if (act < 0 || act >= N) {
     if (lane == 0) { atomicCAS(a.err, 0, ECO_ERR_ARG); a.rewards[e] = 0.0; a.dones[e] = 0; }
     return;
@@ -378,7 +379,15 @@ __global__ __launch_bounds__(256) void env_step_problem_kernel(EnvArgs a) {
   const int gid = sc->graph;
   const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
   const uint32_t* ed = a.gs.edges + a.gs.edge_base[gid];
-  const int sa_old = gsp[act];
+  int s[VPT], F[VPT], tsf[VPT], bs[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v < N) { s[k] = gsp[v]; F[k] = gF[v]; tsf[k] = gt[v]; bs[k] = gb[v]; }
+    else { s[k] = 0; F[k] = 0; tsf[k] = 0; bs[k] = 0; }
+  }
+  int sa_old, Fa;
+  read_vertex<VPT>(s, F, act, sa_old, Fa);
   const int n1_old = sc->n1, inv_old = sc->inv;
   const double qn = sc->qn, mlr = sc->mlr, inorm = sc->inorm;
   // MinDomSet: the action's neighbour counts from the pre-flip state (lanes split its row)
@@ -396,27 +405,12 @@ __global__ __launch_bounds__(256) void env_step_problem_kernel(EnvArgs a) {
     S0a = wave_sum_i(S0a);
     S1a = wave_sum_i(S1a);
   }
-  const FlipDelta fd = flip_delta(tgt, sa_old, gF[act], n1_old, inv_old, S0a, S1a, N, qn, inorm);
+  const FlipDelta fd = flip_delta(tgt, sa_old, Fa, n1_old, inv_old, S0a, S1a, N, qn, inorm);
   const double score = sc->score + fd.d;       // :399
   const double nscore = sc->nscore + fd.dn;    // :400 (accumulated)
-  int s[VPT], F[VPT], tsf[VPT], bs[VPT];
-#pragma unroll
-  for (int k = 0; k < VPT; ++k) {
-    const int v = lane + 64 * k;
-    if (v < N) { s[k] = gsp[v]; F[k] = gF[v]; tsf[k] = gt[v]; bs[k] = gb[v]; }
-    else { s[k] = 0; F[k] = 0; tsf[k] = 0; bs[k] = 0; }
-  }
   // neighbour sums along the row of `act`
-  for (int q = rp[act]; q < rp[act + 1]; ++q) {
-    const uint32_t x = ed[q];
-    const int j = edge_col(x);
-    const int d = field_coef(tgt, edge_w(x)) * sa_old;
-    if ((j & 63) == lane) {
-      const int kk = j >> 6;
-#pragma unroll
-      for (int k = 0; k < VPT; ++k) F[k] += (k == kk) ? d : 0;
-    }
-  }
+  row_update<VPT>(d_lds + wv * N, ed, rp[act], rp[act + 1], N, lane, F,
+                  [&](int w) { return field_coef(tgt, w) * sa_old; });
   uint64_t words[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
