@@ -70,13 +70,24 @@ __device__ __forceinline__ void mds_neighbour_counts(const int32_t* rp, const ui
     const int v = lane + 64 * k;
     int a0 = 0, a1 = 0;
     if (v < N) {
-      for (int q = rp[v]; q < rp[v + 1]; ++q) {
-        const uint32_t x = ed[q];
-        if (edge_w(x) > 0) {
-          const uint8_t c = code[edge_col(x)];
+      const int q1 = rp[v + 1];
+      int q = rp[v];
+      for (; q + 4 <= q1; q += 4) {  // four independent edge loads in flight
+        uint32_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = ed[q + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint8_t c = edge_w(x[u]) > 0 ? code[edge_col(x[u])] : (uint8_t)0;
           a0 += c & 1;
           a1 += c >> 1;
         }
+      }
+      for (; q < q1; ++q) {
+        const uint32_t x = ed[q];
+        const uint8_t c = edge_w(x) > 0 ? code[edge_col(x)] : (uint8_t)0;
+        a0 += c & 1;
+        a1 += c >> 1;
       }
     }
     S0[k] = a0;
