@@ -784,7 +784,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 // and the 8-chunk Linears need more than the 128 VGPRs of a 16-wave workgroup).
 // LDS: Wl [2][64][LDW] | readout scratch
 template <int NW>
-__global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs a, float* hbuf) {
+__global__ __launch_bounds__(64 * NW, 2) void mpnn_forward_large_kernel(MpnnArgs a, float* hbuf) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
@@ -795,8 +795,10 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs
   const int ntiles = rows_pad >> 4;
   const size_t R0 = (size_t)e * N;
   const size_t RT = (size_t)a.B * N;
-  float* Wl = lds;
-  float* Scr = lds + 2 * 64 * LDW;
+  // Linears on the exact bf16x3-split weight fragments streamed from L2 (no LDS weight staging: the
+  // LDS holds only the readout scratch, so two episodes share a CU and hide each other's gathers)
+  const uint16_t* BFP = reinterpret_cast<const uint16_t*>(a.P + PK_BF);
+  float* Scr = lds;
   float* HA = hbuf + (size_t)e * rows_pad * 64 * 3;
   float* HB = HA + (size_t)rows_pad * 64;
   float* EB = HB + (size_t)rows_pad * 64;
@@ -808,8 +810,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs
   const float* x = a.x + R0 * 8;
   auto rinfo = [&](int r) { return row_info_packed(pack_row_info(a, e, r, N)); };
 
-  // ---- phase A: Z = Wx . x into HB; Wf staged ----
-  stage_rows<NT>(Wl, LDH, P + PK_WF, 64, 64, 64);
+  // ---- phase A: Z = Wx . x into HB ----
   {
     float wx[8];
 #pragma unroll
@@ -866,7 +867,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mm_k<4, 4, true>(d, acc, Wl, LDH, lane);
+      mm_bf3_lean(d, acc, BFP + BF_WF, lane);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) st4(EB + (size_t)r * 64 + 16 * nt + 4 * s4, relu4(d[nt]));
     }
@@ -889,15 +890,12 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs
   float* Hc = HA;
   float* Hn = HB;
   for (int layer = 0; layer < 3; ++layer) {
-    const float* Wm = P + PK_LAYER + layer * 16384;
-    stage_rows<NT>(Wl, LDW, Wm, 128, 64, 128);
-    stage_rows<NT>(Wl + 64 * LDW, LDW, Wm + 8192, 128, 64, 128);
-    __syncthreads();
+    const uint16_t* BFL = BFP + BF_LAYER + layer * BF_LAYER_STRIDE;  // message halves, then update halves
     for (int t = w; t < ntiles; t += NW) {
       const int r = t * 16 + c16;
       const bool valid = r < N;
       const RowInfo ri = rinfo(r);
-      float4 am[8];
+      float4 am[4], ev[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) am[c] = zero4();
       for_edges(eg, ri.e0, ri.e1, [&](uint32_t ex) {
@@ -916,27 +914,29 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_forward_large_kernel(MpnnArgs
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         am[c].x = am[c].x / nf; am[c].y = am[c].y / nf; am[c].z = am[c].z / nf; am[c].w = am[c].w / nf;
-        am[4 + c] = f4(EB + (size_t)r * 64 + 16 * c + 4 * s4);
+        ev[c] = f4(EB + (size_t)r * 64 + 16 * c + 4 * s4);
       }
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mm_k<4, 8, true>(d, am, Wl, LDW, lane);
-      float4 au[8];
+      mm_bf3_lean(d, am, BFL, lane);             // message = relu(Wm . [agg, e])
+      mm_bf3_lean(d, ev, BFL + BF_HALF, lane);
+      float4 hc[4], mr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        au[c] = f4(Hc + (size_t)r * 64 + 16 * c + 4 * s4);
-        au[4 + c] = relu4(d[c]);
+        hc[c] = f4(Hc + (size_t)r * 64 + 16 * c + 4 * s4);
+        mr[c] = relu4(d[c]);
       }
       f32x4 hn[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mm_k<4, 8, true>(hn, au, Wl + 64 * LDW, LDW, lane);
+      mm_bf3_lean(hn, hc, BFL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+      mm_bf3_lean(hn, mr, BFL + 3 * BF_HALF, lane);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) st4(Hn + (size_t)r * 64 + 16 * nt + 4 * s4, valid ? relu4(hn[nt]) : zero4());
     }
     __threadfence();  // release the Hn rows and invalidate this CU's L1 before other waves read them
-    __syncthreads();  // every wave done with Hc, Wl; Hn complete
+    __syncthreads();  // every wave done with Hc; Hn complete
     float* tmp = Hc;
     Hc = Hn;
     Hn = tmp;
@@ -1091,7 +1091,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
     const int rows_pad = (N + 15) & ~15;
-    const size_t lds = ((size_t)2 * 64 * LDW + readout_scratch_floats(rows_pad, 1, 8, true)) * sizeof(float);
+    const size_t lds = (size_t)readout_scratch_floats(rows_pad, 1, 8, true) * sizeof(float);
     (void)hipFuncSetAttribute((const void*)mpnn_forward_large_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     mpnn_forward_large_kernel<8><<<batch, 512, lds, st>>>(a, (float*)((char*)workspace + 256));
