@@ -58,6 +58,35 @@ def load_graph(graph_dir, graph_name, dense=True):
     return Graph(graph_name, n, m, matrix, bk_val, bk_sol)
 
 
+def load_graph_set(graph_save_loc):
+    """experiments/utils.py:420-432: a pickled list of graphs (networkx Graphs, scipy CSR matrices or dense
+    arrays, as the reference's `_graphs/*.pkl` test sets) -> list of dense f64 adjacency arrays.
+    Unpickling executes code from the file: load only graph sets you trust (e.g. ones written by
+    `save_graph_set`).  `GraphStore.from_dense(load_graph_set(path))` puts them on the device."""
+    import pickle
+    with open(graph_save_loc, "rb") as f:
+        graphs = pickle.load(f)
+
+    def to_array(g):
+        if type(g).__module__.startswith("networkx"):
+            import networkx as nx
+            return nx.to_numpy_array(g)
+        if hasattr(g, "toarray"):  # scipy.sparse
+            return g.toarray()
+        return np.asarray(g, dtype=np.float64)
+
+    graphs = [to_array(g) for g in graphs]
+    print('{} target graphs loaded from {}'.format(len(graphs), graph_save_loc))
+    return graphs
+
+
+def save_graph_set(graph_save_loc, graphs):
+    """Write a graph set in the reference's pickle format (a list of dense adjacency arrays)."""
+    import pickle
+    with open(graph_save_loc, "wb") as f:
+        pickle.dump([np.asarray(g, dtype=np.float64) for g in graphs], f)
+
+
 def _greedy(env):
     """Run the batched Greedy solver (solver.py:88-131) to completion on `env` (already reset)."""
     for _ in range(env.max_steps):

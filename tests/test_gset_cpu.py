@@ -56,3 +56,26 @@ def test_edges_to_csr_equals_dense_to_csr():
     rp2, _, e2 = dense_to_csr([m])
     np.testing.assert_array_equal(rp1, rp2)
     np.testing.assert_array_equal(e1, e2)
+
+
+def test_graph_set_pickle_round_trip(tmp_path):
+    """load_graph_set (experiments/utils.py:420-432) on a graph set written here: dense arrays, scipy CSR
+    and networkx graphs all come back as the dense f64 adjacency."""
+    import pickle
+    import networkx as nx
+    import scipy.sparse as sp
+    from eco_hip.experiments import load_graph_set, save_graph_set
+    rng = np.random.default_rng(0)
+    mats = []
+    for _ in range(3):
+        a = np.triu((rng.random((12, 12)) < 0.3).astype(np.float64), 1)
+        mats.append(a + a.T)
+    p = tmp_path / "set.pkl"
+    save_graph_set(str(p), mats)
+    back = load_graph_set(str(p))
+    assert len(back) == 3 and all(np.array_equal(a, b) for a, b in zip(mats, back))
+    q = tmp_path / "mixed.pkl"
+    with open(q, "wb") as f:
+        pickle.dump([sp.csr_matrix(mats[0]), nx.from_numpy_array(mats[1]), mats[2]], f)
+    back = load_graph_set(str(q))
+    assert all(np.array_equal(a, b) for a, b in zip(mats, back))
