@@ -1,6 +1,7 @@
 // Shared layout constants of the MPNN kernels (forward/backward, eco_train.hip).
 #pragma once
 #include "eco_common.h"
+#include <cstdlib>
 
 namespace eco {
 
@@ -104,7 +105,31 @@ enum { GR_DUU0 = 0, GR_DUU1, GR_DUU2, GR_DUM0, GR_DUM1, GR_DUM2, GR_DUE, GR_DU0,
        GR_NODE_TENSORS };  // then DP [B][64], DWRA [B][64], DWRB [B][64], DBR [B(pad 64)], DWA [nblocks][64]
 
 // whole graphs per workgroup block: up to 208 rows (13 tiles) share the LDS-resident embeddings
-inline int graphs_per_block(int N) { return N >= 208 ? 1 : 208 / N; }
+// Graphs per workgroup block for B graphs of N vertices (every MPNN launch and workspace size of a call
+// uses the same value).  Up to 208 rows per block; within that, the count whose launch is estimated
+// fastest: rounds of blocks over the CUs x (16-row tiles per SIMD + 1 for the block's staging and
+// readout) -- e.g. ER-20 x4096: 8 graphs (10 tiles, 512 blocks) beats 10 (13 tiles, 410 blocks) by 16 %.
+inline int graphs_per_block(int N, int B) {
+  static const int cap = [] { const char* e = getenv("ECO_MPNN_GPB"); return e ? atoi(e) : 0; }();  // A/B knob
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess || n < 1)
+      n = 256;
+    return n;
+  }();
+  const int gmax = N >= 208 ? 1 : 208 / N;
+  if (cap > 0) return cap < gmax ? cap : gmax;
+  int best = gmax;
+  double best_cost = 1e300;
+  for (int g = gmax; g >= 1 && 2 * g >= gmax; --g) {
+    const int tiles = (g * N + 15) / 16;
+    const long long blocks = ((long long)B + g - 1) / g;
+    const double cost = (double)((blocks + cus - 1) / cus) * ((tiles + 3) / 4 + 1);
+    if (cost < best_cost) { best_cost = cost; best = g; }
+  }
+  return best;
+}
 
 // dense-path bitmask adjacency of graphs [first, first + count) into gs->adjbits (eco_mpnn_dense.h)
 int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st);

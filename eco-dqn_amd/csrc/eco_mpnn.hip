@@ -962,7 +962,7 @@ static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco
   if (norm_scope != ECO_NORM_PER_GRAPH && norm_scope != ECO_NORM_PER_CALL)
     return fail(ECO_ERR_ARG, "bad norm_scope");
   a = MpnnArgs{};
-  a.P = packed; a.gs = *gs; a.gids = graph_ids; a.B = batch; a.N = N; a.gpb = graphs_per_block(N);
+  a.P = packed; a.gs = *gs; a.gids = graph_ids; a.B = batch; a.N = N; a.gpb = graphs_per_block(N, batch);
   a.nobs = n_obs_in; a.xw = ECO_OBS_X_STRIDE(n_obs_in); a.x = obs_x; a.norm_scope = norm_scope;
   if (a.xw != 8 && N > MPNN_MAX_SPINS)
     return fail(ECO_ERR_ARG, "more than 8 node features need N <= 512 (the N > 512 kernel takes 8-float rows)");
@@ -1123,7 +1123,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
 
 size_t eco::mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch) {
   if (n_spins < 1 || batch < 1) return 0;
-  const int gpb = graphs_per_block(n_spins);
+  const int gpb = graphs_per_block(n_spins, batch);
   const size_t nblk = (batch + gpb - 1) / gpb;
   return ((size_t)GR_NODE_TENSORS * n_spins * batch * 64 + 3 * (size_t)batch * 64 + (((size_t)batch + 63) & ~63ull) +
           nblk * 64) * sizeof(float);

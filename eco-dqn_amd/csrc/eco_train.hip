@@ -313,7 +313,7 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   const float* DWRB = DWRA + (size_t)batch * 64;
   const float* DBR = DWRB + (size_t)batch * 64;
   const float* DWA = DBR + (((size_t)batch + 63) & ~63ull);
-  const int gpb = graphs_per_block(N);
+  const int gpb = graphs_per_block(N, batch);
   const int nblk = (batch + gpb - 1) / gpb;
   float* slabs = (float*)((char*)workspace + align_up(mpnn_grad_ws_bytes(N, batch), 256));
   const FlatOffsets fo = flat_offsets(n_obs_in);
