@@ -143,6 +143,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
   int2* RI = reinterpret_cast<int2*>(Mreg + fwd_mreg_floats(rows_pad, a.gpb, NW, WLDS));
   int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);  // [gpb] per-graph edge base
   int* MD = reinterpret_cast<int*>(GB + a.gpb);               // [gpb] per-graph max degree
+  int* SCH = MD + ((a.gpb + 1) & ~1);                           // [64] tile schedule
   float* Es = WLDS ? Wl : Mreg;     // phase-E scratch
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
@@ -187,6 +188,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
   }
   if constexpr (WLDS) stage_rows<NT>(Wl, LDH, P + PK_WF, 64, 64, 64);
   __syncthreads();
+  if (w == 0) build_tile_schedule(SCH, RI, ntiles, NW, MAXT);  // published by the barrier after phase A
   ECO_TS(1);
 
   // ---- phase A: Z = Wx . x  (edge-embedding node term) into Hs ----
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
       for (int i = 0; i < 4; ++i) wa[c * 4 + i] = P[PK_WA + 16 * c + 4 * s4 + i];
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NW;
+      const int t = SCH[w + ti * NW];
       if (t >= ntiles) break;
       const int r = t * 16 + c16;
       const RowInfo ri = row_info(RI, r);
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
     f32x4 hn[MAXT][4];
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NW;
+      const int t = SCH[w + ti * NW];
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const RowInfo ri = row_info(RI, r);
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_forwa
     __syncthreads();
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NW;
+      const int t = SCH[w + ti * NW];
       if (t < ntiles) {
         const int r = t * 16 + c16;
 #pragma unroll
@@ -437,6 +439,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
   int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
   float* DMEAN = reinterpret_cast<float*>(GB + a.gpb);
   float* RED = DMEAN + a.gpb * 64;
+  int* SCH = reinterpret_cast<int*>(RED + (a.gpb < NW ? a.gpb : 1) * NW * 64);  // [64] tile schedule
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
   const float* P = a.P;
@@ -469,6 +472,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
     }
   }
   __syncthreads();
+  if (w == 0) build_tile_schedule(SCH, RI, ntiles, NWAVE, MAXT);  // published by the barrier after the readout
   ECO_TS(17);
 
   // ---- readout backward (mpnn.py:143-159) ----
@@ -520,7 +524,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
   float4 dh[MAXT][4];
 #pragma unroll
   for (int ti = 0; ti < MAXT; ++ti) {
-    const int t = w + ti * NWAVE;
+    const int t = SCH[w + ti * NWAVE];
     const int r = t * 16 + c16;
 #pragma unroll
     for (int c = 0; c < 4; ++c) dh[ti][c] = zero4();
@@ -555,7 +559,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
     }
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
+      const int t = SCH[w + ti * NWAVE];
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
     // dh_l = dh_direct + A^T . (dagg / norm)   (A symmetric: a gather over the node's own row)
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
+      const int t = SCH[w + ti * NWAVE];
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
@@ -631,7 +635,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
   // ---- h0 = relu(W0.x): du0 ----
 #pragma unroll
   for (int ti = 0; ti < MAXT; ++ti) {
-    const int t = w + ti * NWAVE;
+    const int t = SCH[w + ti * NWAVE];
     const int r = t * 16 + c16;
     if (t < ntiles && r < rows_valid) {
       const float* h0 = SV(SV_H0) + (R0 + r) * 64 + 4 * s4;
@@ -652,7 +656,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
   }
 #pragma unroll
   for (int ti = 0; ti < MAXT; ++ti) {
-    const int t = w + ti * NWAVE;
+    const int t = SCH[w + ti * NWAVE];
     if (t < ntiles) {
       const int r = t * 16 + c16;
       const bool valid = r < rows_valid;
@@ -692,7 +696,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
     for (int i = 0; i < 16; ++i) dwa[i] = 0.f;
 #pragma unroll
     for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NWAVE;
+      const int t = SCH[w + ti * NWAVE];
       if (t < ntiles) {
         const int r = t * 16 + c16;
         const bool valid = r < rows_valid;
@@ -1020,11 +1024,11 @@ static size_t lds_bytes(int rows_pad, int gpb, int nw, bool wlds, bool backward)
   if (backward) {
     if (wlds) f += (size_t)2 * 128 * LDH + (size_t)rows_pad * 8;  // Wu^T, Wm^T + x rows
     f += (size_t)rows_pad * 2 + 2 * (size_t)gpb;               // packed row info + per-graph edge base
-    f += (size_t)gpb * 64 + (size_t)(gpb < nw ? gpb : 1) * nw * 64;
+    f += (size_t)gpb * 64 + (size_t)(gpb < nw ? gpb : 1) * nw * 64 + 64;  // + tile schedule
   } else {
     if (wlds) f += (size_t)2 * 64 * LDW;
     f += (size_t)fwd_mreg_floats(rows_pad, gpb, nw, wlds);
-    f += (size_t)rows_pad * 2 + 3 * (size_t)gpb;  // packed row info + per-graph edge base, max degree
+    f += (size_t)rows_pad * 2 + 3 * (size_t)gpb + 2 + 64;  // row info, edge base, max degree, tile schedule
   }
   return f * sizeof(float);
 }

@@ -117,6 +117,34 @@ __device__ __forceinline__ RowInfo row_info(const int2* RI, int r) {
   return RowInfo{p.x, p.x + (p.y & 0xFFFF), p.y >> 16};
 }
 
+// Balanced tile schedule of the CSR-gather kernels, built by one wave once the row info RI is staged:
+// SCH[v] = the 16-row tile that virtual slot v = w + ti * nw (wave w's ti-th tile) processes, or ntiles
+// for an empty slot.  A tile's gathers run as long as its largest degree, and preferential-attachment
+// graphs put their hubs in the first tiles; so the tiles are ranked by that cost (descending, index on
+// ties) and the ranks dealt to the waves in a snake (ti even: rank ti*nw + w, odd: ti*nw + nw-1-w), which
+// pairs each wave's heavy tile with light ones.  ntiles <= 64 and ntiles <= nw * maxt.
+__device__ __forceinline__ void build_tile_schedule(int* SCH, const int2* RI, int ntiles, int nw, int maxt) {
+  const int lane = threadIdx.x & 63;
+  int cost = -1;
+  if (lane < ntiles) {
+    cost = 0;
+    for (int i = 0; i < 16; ++i) cost = max(cost, RI[lane * 16 + i].y & 0xFFFF);
+  }
+  int rank = 0;
+  for (int u = 0; u < ntiles; ++u) {
+    const int cu = __shfl(cost, u, 64);
+    rank += (cu > cost) || (cu == cost && u < lane);
+  }
+  for (int v = lane; v < nw * maxt; v += 64) SCH[v] = ntiles;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < ntiles) {
+    const int ti = rank / nw, j = rank - ti * nw;
+    SCH[((ti & 1) ? nw - 1 - j : j) + ti * nw] = lane;
+  }
+}
+
 // Visit the packed edges [e0, e1): groups of 4 edge words, the next group's loads issued before
 // the current group is consumed (one exposed load latency per 4 edges instead of per edge).
 template <typename F>
