@@ -1,6 +1,6 @@
 // DQN training hot path on gfx950 (src/agents/dqn/dqn.py:403-451, dqn/utils.py:28-83):
 // device replay ring, double-DQN TD target + MSE gradient, MPNN weight gradients
-// (split-K reductions over every node of the minibatch on v_mfma_f32_32x32x2_f32,
+// (split-K reductions over every node of the minibatch on bf16x3-split v_mfma_f32_32x32x16_bf16,
 // per-wave partial slabs reduced in a fixed order -> bitwise reproducible), Adam.
 #include <cmath>
 
@@ -31,6 +31,7 @@ constexpr int LDY = 68, LDX = 132;         // padded LDS row strides
 struct WJobs {
   WJob j[MAX_JOBS];
   int n;
+  int nwg;  // workgroups (= slabs) per job, <= WG_PER_JOB
 };
 
 // One workgroup (4 waves) reduces a contiguous row range of one job: 32-row tiles of dY and
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
   const int K = J.K1 + J.K2;
   const int K4 = (K + 3) & ~3;
   const int ntile = 2 * ((K + 31) / 32);
-  const int chunk = ((J.R + WG_PER_JOB - 1) / WG_PER_JOB + WROWS - 1) / WROWS * WROWS;
+  const int chunk = ((J.R + jobs.nwg - 1) / jobs.nwg + WROWS - 1) / WROWS * WROWS;
   const int r0 = blockIdx.x * chunk;
   const int r1 = min(J.R, r0 + chunk);
   f32x16 acc[2];
@@ -132,6 +133,167 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
   }
 }
 
+// Same reduction on 32x32x16 bf16 MFMAs: dY and X are split EXACTLY into three bf16 pieces while a
+// 32-row tile is staged (split3_bits), and the six products above 2^-24 relative are accumulated in
+// f32 (as mm_bf3 does for the forward Linears), so the sums keep f32 accuracy at ~2.7x the f32-MFMA
+// rate.  Staging transposes through registers: thread t loads column (t & 63) of 8 consecutive rows
+// (each wave-level load is one contiguous 256-B row segment), splits, and writes the three 8-row
+// pieces as 16-B LDS stores into [p][column][row] planes, which are exactly the MFMA fragments
+// (lane l: column l & 31, rows 8 (l >> 5) .. +7 of a 16-row k-step).
+constexpr int WB_LD = 40;  // bf16 per plane column (32 rows + 8 pad: 80-B stride, conflict-light 16-B reads)
+typedef short bf16x8w __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split8_store(uint16_t* base, int plane_stride, const float (&v)[8]) {
+  u32x4w p1, p2, p3;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    uint16_t a0, b0, c0, a1, b1, c1;
+    split3_bits(v[2 * t], a0, b0, c0);
+    split3_bits(v[2 * t + 1], a1, b1, c1);
+    p1[t] = a0 | (uint32_t)a1 << 16;
+    p2[t] = b0 | (uint32_t)b1 << 16;
+    p3[t] = c0 | (uint32_t)c1 << 16;
+  }
+  *reinterpret_cast<u32x4w*>(base) = p1;
+  *reinterpret_cast<u32x4w*>(base + plane_stride) = p2;
+  *reinterpret_cast<u32x4w*>(base + 2 * plane_stride) = p3;
+}
+
+__global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs) {
+  constexpr int PY = 64 * WB_LD, PX = 128 * WB_LD;  // plane strides (bf16)
+  __shared__ __attribute__((aligned(16))) uint16_t sY[3 * PY];
+  __shared__ __attribute__((aligned(16))) uint16_t sX[3 * PX];
+  const WJob& J = jobs.j[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int jj = lane & 31, h = lane >> 5;
+  const int K = J.K1 + J.K2;
+  const int ntile = 2 * ((K + 31) / 32);
+  const int chunk = ((J.R + jobs.nwg - 1) / jobs.nwg + WROWS - 1) / WROWS * WROWS;
+  const int r0 = blockIdx.x * chunk;
+  const int r1 = min(J.R, r0 + chunk);
+  // staging roles: dY column yc of rows 8 yg .. +7; X columns xc (+ 0 / 1 x 128 units) of rows 8 xg .. +7
+  const int yc = threadIdx.x & 63, yg = threadIdx.x >> 6;
+  const int xc = threadIdx.x & 127, xg0 = threadIdx.x >> 7;  // units u = t + 256 k: column u & 127, group u >> 7
+  typedef const __attribute__((address_space(1))) float gfloat;
+  // loads are unconditional (rows clamped to r1 - 1, dead columns read column 0) and masked after:
+  // predicated loads compiled to one branch + vmcnt(0) wait per row, serialising the whole tile
+  const bool xlive = xc < K;
+  gfloat* ysrc = (gfloat*)(J.dY + yc);
+  const float* xsrc = !xlive ? J.X1 : (xc < J.K1 ? J.X1 + xc : J.X2 + (xc - J.K1));
+  int xld = xlive && xc >= J.K1 ? J.ld2 : J.ld1;
+  uint32_t xmask = xlive ? 0xFFFFFFFFu : 0u;
+  // keep the per-lane source and mask opaque (otherwise the select is sunk into every load as a branch)
+  asm volatile("" : "+v"(xsrc), "+v"(xld), "+v"(xmask));
+  gfloat* xg = (gfloat*)xsrc;
+  const int rlast = r1 - 1;
+  f32x16 acc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
+  // two register buffers: tiles i+1 and i+2 are in flight while tile i is split and multiplied
+  // (one tile in flight held the reduction at ~4 TB/s: too few bytes outstanding per CU)
+  struct Regs {
+    float y[8], x[2][8];
+  };
+  // raw loads only; the row / column masks are applied when the tile is stored (masking at load
+  // time makes the compiler wait for every load before the multiply it should overlap)
+  auto load_tile = [&](Regs& R, int rb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + 2 * u) + k, rlast) * (size_t)xld];
+  };
+  auto store_tile = [&](Regs& R, int rb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
+    split8_store(sY + yc * WB_LD + 8 * yg, PY, R.y);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        R.x[u][k] = rb + 8 * (xg0 + 2 * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
+      split8_store(sX + xc * WB_LD + 8 * (xg0 + 2 * u), PX, R.x[u]);
+    }
+  };
+  // this wave's output tiles: t = w + 4q -> o-tile w & 1, i-tiles (w >> 1) and (w >> 1) + 2
+  const int ot = w & 1;
+  const bool live0 = w < ntile, live1 = w + 4 < ntile;
+  const uint16_t* ya = sY + (32 * ot + jj) * WB_LD + 8 * h;
+  const uint16_t* xb0 = sX + (32 * (w >> 1) + jj) * WB_LD + 8 * h;
+  const uint16_t* xb1 = xb0 + 64 * WB_LD;
+  auto compute = [&]() {
+  if (live0) {
+#pragma unroll
+    for (int s = 0; s < WROWS / 16; ++s) {
+      const bf16x8w a1 = *reinterpret_cast<const bf16x8w*>(ya + 16 * s);
+      const bf16x8w a2 = *reinterpret_cast<const bf16x8w*>(ya + PY + 16 * s);
+      const bf16x8w a3 = *reinterpret_cast<const bf16x8w*>(ya + 2 * PY + 16 * s);
+      const bf16x8w b1 = *reinterpret_cast<const bf16x8w*>(xb0 + 16 * s);
+      const bf16x8w b2 = *reinterpret_cast<const bf16x8w*>(xb0 + PX + 16 * s);
+      const bf16x8w b3 = *reinterpret_cast<const bf16x8w*>(xb0 + 2 * PX + 16 * s);
+      if (live1) {
+        const bf16x8w c1 = *reinterpret_cast<const bf16x8w*>(xb1 + 16 * s);
+        const bf16x8w c2 = *reinterpret_cast<const bf16x8w*>(xb1 + PX + 16 * s);
+        const bf16x8w c3 = *reinterpret_cast<const bf16x8w*>(xb1 + 2 * PX + 16 * s);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, c1, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, c2, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, c3, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, c1, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, c2, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, c1, acc[1], 0, 0, 0);
+      } else {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b3, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b1, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b2, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[0], 0, 0, 0);
+      }
+    }
+  }
+  };
+  Regs RA, RB;
+  if (r0 < r1) load_tile(RA, r0);
+  if (r0 + WROWS < r1) load_tile(RB, r0 + WROWS);
+  for (int rb = r0; rb < r1; rb += 2 * WROWS) {
+    store_tile(RA, rb);
+    __syncthreads();
+    if (rb + 2 * WROWS < r1) load_tile(RA, rb + 2 * WROWS);
+    compute();
+    __syncthreads();
+    if (rb + WROWS >= r1) break;
+    store_tile(RB, rb + WROWS);
+    __syncthreads();
+    if (rb + 3 * WROWS < r1) load_tile(RB, rb + 3 * WROWS);
+    compute();
+    __syncthreads();
+  }
+  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x) * SLAB;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int t = w + 4 * q;
+    if (t < ntile) {
+      const int it = t >> 1;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
+        slab[o * 128 + 32 * it + jj] = acc[q][k];
+      }
+    }
+  }
+}
+
 // fixed-order sum of the slabs of every job into the flat gradient
 __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad) {
   const WJob& J = jobs.j[blockIdx.y];
@@ -141,7 +303,7 @@ __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad)
   if (o >= J.nO || i >= K) return;
   const float* s = slabs + (size_t)blockIdx.y * SLABS_PER_JOB * SLAB + o * 128 + i;
   float acc = 0.f;
-  for (int k = 0; k < SLABS_PER_JOB; ++k) acc += s[(size_t)k * SLAB];
+  for (int k = 0; k < jobs.nwg; ++k) acc += s[(size_t)k * SLAB];
   grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
 }
 
@@ -331,7 +493,15 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, xw, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
-  wgrad_kernel<<<dim3(WG_PER_JOB, n), 256, 0, st>>>(J, slabs);
+  static const bool f32_wgrad = getenv("ECO_WGRAD_F32") != nullptr;  // A/B switch: the f32-MFMA reduction
+  if (f32_wgrad) {
+    J.nwg = WG_PER_JOB;
+    wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
+  } else {
+    // 46 KB LDS -> 3 workgroups per CU: one resident wave of workgroups over the 256 CUs
+    J.nwg = std::min(WG_PER_JOB, 3 * 256 / n);
+    wgrad_bf3_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
+  }
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
   colsum_kernel<<<64, 256, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
   colsum_kernel<<<64, 256, 0, st>>>(DWRB, batch, 64, 64, grad + fo.Wr + 64, 1);
