@@ -85,7 +85,31 @@ def cpu_baseline(n=200, seconds=12.0, train=True):
                        f"(numpy SpinSystem restatement + torch-CPU MPNN, B=1)")
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v3", "pmc_hbm.json")
+def cpu_env_step_baseline(n=200, seconds=4.0):
+    """Oracle (CPU 'port') SpinSystem.step alone with a uniform random policy (configs[0]'s plumbing
+    loop, spinsystem.py:355-559), one core: only env.step is timed (graph generation and reset are
+    not).  The oracle's vectorised step runs ~1.5x the reference's own measured ER-200 rate here
+    (2,227/s), so this baseline flatters the CPU."""
+    sys.path.insert(0, REPO)
+    from oracle import spinsystem_oracle as so
+    from oracle import graphs as og
+    rng = np.random.default_rng(0)
+    steps, busy = 0, 0.0
+    while busy < seconds:
+        env = so.SpinSystemOracle(og.er_graph(n, 0.15, rng), 2 * n, basin_reward=1. / n)
+        env.reset(rng=np.random.RandomState(int(rng.integers(1 << 31))))
+        acts = rng.integers(0, n, 2 * n)
+        t0 = time.perf_counter()
+        for a in acts:
+            env.step(int(a))
+        busy += time.perf_counter() - t0
+        steps += 2 * n
+    return dict(value=steps / busy, unit="env-steps/s", cores=1, kind="port",
+                sample=f"{steps} ER-{n} env.step calls ({steps // (2 * n)} episodes of T=2N, random actions) in "
+                       f"{busy:.1f}s, numpy SpinSystem restatement, 1 thread")
+
+
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v4", "pmc_hbm.json")
 
 
 def pmc_traffic(dom, B, M, n, graph="ER"):
@@ -107,7 +131,7 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
             return (act["hbm_bytes_per_launch"] + 3 * (B * 2 // M) * tr["hbm_bytes_per_launch"]) / \
                 (1 + 3 * (B * 2 // M))
         bw = k["mpnn_backward_dense_kernel"][str((M + gpb - 1) // gpb)]
-        wg = next(iter(k["wgrad_kernel"].values()))
+        wg = next(iter(k.get("wgrad_bf3_kernel", k.get("wgrad_kernel")).values()))
         return bw["hbm_bytes_per_launch"] + wg["hbm_bytes_per_launch"]
     except (KeyError, StopIteration):
         return None
@@ -248,13 +272,15 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v3/pmc_hbm.json)",
+                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v4/pmc_hbm.json)",
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(n, train=train)
+            if args.graph == "ER":
+                out["cpu_baseline_env_step"] = cpu_env_step_baseline(n)
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()
