@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
       for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + 2 * u) + k, rlast) * (size_t)xld];
   };
   auto store_tile = [&](Regs& R, int rb) {
+    asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
 #pragma unroll
     for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
     split8_store(sY + yc * WB_LD + 8 * yg, PY, R.y);
@@ -263,21 +264,25 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
     }
   }
   };
-  Regs RA, RB;
-  if (r0 < r1) load_tile(RA, r0);
-  if (r0 + WROWS < r1) load_tile(RB, r0 + WROWS);
-  for (int rb = r0; rb < r1; rb += 2 * WROWS) {
-    store_tile(RA, rb);
-    __syncthreads();
-    if (rb + 2 * WROWS < r1) load_tile(RA, rb + 2 * WROWS);
-    compute();
-    __syncthreads();
-    if (rb + WROWS >= r1) break;
-    store_tile(RB, rb + WROWS);
-    __syncthreads();
-    if (rb + 3 * WROWS < r1) load_tile(RB, rb + 3 * WROWS);
-    compute();
-    __syncthreads();
+  // loads are issued unconditionally (rows past r1 clamp to r1 - 1 and are masked at the store): a
+  // conditional load makes the compiler drain every tile in flight at the join (vmcnt(0))
+  if (r0 < r1) {
+    Regs RA, RB;
+    load_tile(RA, r0);
+    load_tile(RB, r0 + WROWS);
+    for (int rb = r0; rb < r1; rb += 2 * WROWS) {
+      store_tile(RA, rb);
+      __syncthreads();
+      load_tile(RA, rb + 2 * WROWS);
+      compute();
+      __syncthreads();
+      if (rb + WROWS >= r1) break;
+      store_tile(RB, rb + WROWS);
+      __syncthreads();
+      load_tile(RB, rb + 3 * WROWS);
+      compute();
+      __syncthreads();
+    }
   }
   float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x) * SLAB;
 #pragma unroll
