@@ -790,7 +790,6 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 template <int NW>
 __global__ __launch_bounds__(64 * NW, 2) void mpnn_forward_large_kernel(MpnnArgs a, float* hbuf) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int e = blockIdx.x;
