@@ -85,28 +85,52 @@ def cpu_baseline(n=200, seconds=12.0, train=True):
                        f"(numpy SpinSystem restatement + torch-CPU MPNN, B=1)")
 
 
-def cpu_env_step_baseline(n=200, seconds=4.0):
-    """Oracle (CPU 'port') SpinSystem.step alone with a uniform random policy (configs[0]'s plumbing
-    loop, spinsystem.py:355-559), one core: only env.step is timed (graph generation and reset are
-    not).  The oracle's vectorised step runs ~1.5x the reference's own measured ER-200 rate here
-    (2,227/s), so this baseline flatters the CPU."""
-    sys.path.insert(0, REPO)
-    from oracle import spinsystem_oracle as so
-    from oracle import graphs as og
-    rng = np.random.default_rng(0)
-    steps, busy = 0, 0.0
-    while busy < seconds:
-        env = so.SpinSystemOracle(og.er_graph(n, 0.15, rng), 2 * n, basin_reward=1. / n)
-        env.reset(rng=np.random.RandomState(int(rng.integers(1 << 31))))
-        acts = rng.integers(0, n, 2 * n)
-        t0 = time.perf_counter()
-        for a in acts:
-            env.step(int(a))
-        busy += time.perf_counter() - t0
-        steps += 2 * n
-    return dict(value=steps / busy, unit="env-steps/s", cores=1, kind="port",
-                sample=f"{steps} ER-{n} env.step calls ({steps // (2 * n)} episodes of T=2N, random actions) in "
-                       f"{busy:.1f}s, numpy SpinSystem restatement, 1 thread")
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return next(ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        import platform
+        return platform.processor() or platform.machine()
+
+
+def cpu_refcost_baseline(n=200, seconds=10.0):
+    """SURVEY.md 8d CPU side-by-side: the reference-cost restatement of env.step (oracle/refcost.py:
+    the reference's per-step op mix -- 4 dense J@s matvecs, 2 dense np.outer cuts, the observables
+    loop, the list-of-sets visited buffer and the vstack observation; bit-exact with the reference
+    and calibrated against it in the build container, oracle/refcost_calibration.json) with a
+    uniform random policy (configs[0]'s plumbing loop) on fresh ER(n, 0.15) graphs, one single-
+    threaded process per host core of this job's CPU share (at most 16 per GPU on the box), all at
+    once.  value = the sum of the per-process rates; only env.step is timed."""
+    import subprocess
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    procs = max(1, min(share, int(os.environ.get("ECO_CPU_BASELINE_PROCS", "16"))))
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, "-m", "oracle.refcost", str(n), str(seconds), str(100 + i)], cwd=REPO,
+                           env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+          for i in range(procs)]
+    rates, steps = [], 0
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds * 6 + 120)
+        st, busy = out.split()
+        steps += int(st)
+        rates.append(int(st) / float(busy))
+    cal = None
+    try:
+        with open(os.path.join(REPO, "oracle", "refcost_calibration.json")) as fh:
+            cal = {c["workload"]: round(c["ratio"], 3) for c in json.load(fh)["cases"]}
+    except (OSError, ValueError, KeyError):
+        pass
+    return dict(value=float(sum(rates)), unit="env-steps/s", cores=procs, kind="port",
+                nproc=os.cpu_count(), cpu_share=share, cpu_model=_cpu_model(),
+                per_core=float(np.mean(rates)),
+                sample=f"{steps} ER-{n} env.step calls (random actions, T=2N episodes) in {procs} single-threaded "
+                       f"processes x {seconds:.0f}s of oracle/refcost.py, the reference-cost restatement of "
+                       "spinsystem.py:355-574",
+                calibration_ratio_vs_reference=cal)
 
 
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v4", "pmc_hbm.json")
@@ -137,9 +161,111 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
         return None
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(nproc):
+    """`bench.py --gpus N` without a torch.distributed.run environment: start N fresh child
+    processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT set (one process per GPU, episodes sharded).  The parent never
+    touches the GPU (no torch.cuda call before or after the children start; nothing is exec'd);
+    children inherit stdout, and only rank 0 prints the JSON line.  A failing rank stops the
+    others; the parent exits with the first non-zero code."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:  # one rank failed: the collective would hang the rest
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run_bench(args, world, rank, local):
+    """--dry-run: the launcher / rendezvous / timing harness on CPU over gloo (no GPU).  A step is a
+    small numpy reduction; rank 0 reports the world size the process group observed and every rank's
+    local rank, so a CPU test can check that N distinct ranks ran and exactly one line was printed."""
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+    if os.environ.get("ECO_BENCH_DRY_FAIL_RANK") == str(rank):
+        raise SystemExit(3)  # failure-propagation check of the launcher
+    x = np.random.default_rng(rank).random(1 << 16)
+    for _ in range(args.warmup):
+        float(x.sum())
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        float(x.sum())
+    if world > 1:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    per_rank = _gather_floats([dt, float(local)], world)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher check)", "value": 0.0, "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": max(p[0] for p in per_rank) / max(args.steps, 1) * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic", "config": {"workload": "dry-run"},
+                          "process_group": {"backend": "gloo" if world > 1 else None, "world_size": world,
+                                            "local_ranks": [int(p[1]) for p in per_rank]}}))
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+def _gather_floats(vals, world, device=None):
+    """All-gather a short list of floats from every rank (rank-ordered list of lists)."""
+    if world == 1:
+        return [list(vals)]
+    import torch.distributed as tdist
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    tdist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
+def process_group_info(world, per_rank_s, steps, local, device):
+    """What the collective backend saw: its name and world size, and every rank's own timed-region
+    ms per step (the headline ms_per_step is the max over ranks)."""
+    import torch.distributed as tdist
+    ranks = _gather_floats([per_rank_s / max(steps, 1) * 1e3, float(local)], world, device)
+    ms = [r[0] for r in ranks]
+    return {"backend": tdist.get_backend() if world > 1 else None,
+            "rccl_world_size": tdist.get_world_size() if world > 1 else 1,
+            "local_ranks": [int(r[1]) for r in ranks],
+            "ms_per_step_min": min(ms), "ms_per_step_max": max(ms)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; N > 1 without a torch.distributed.run environment starts N ranks")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only launcher/rendezvous check over gloo (no GPU work)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=8192)
@@ -160,9 +286,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run_bench(args, world, rank, local)
     dist = world > 1
     if dist:
         torch.cuda.set_device(local)
@@ -171,9 +301,9 @@ def main():
     torch.cuda.set_device(dev)
 
     if args.workload in ("gset", "er20"):
-        return inference_bench(args, world, rank, dev, dist)
+        return inference_bench(args, world, rank, local, dev, dist)
     if args.workload == "envstep":
-        return envstep_bench(args, world, rank, dev, dist)
+        return envstep_bench(args, world, rank, local, dev, dist)
 
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
@@ -225,11 +355,12 @@ def main():
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt_rank = time.perf_counter() - t0
     agent.network.timer = None
     agent.target_network.timer = None
     from eco_hip.parallel import max_over_ranks
-    dt = max_over_ranks(dt, device=dev)
+    dt = max_over_ranks(dt_rank, device=dev)
+    pg = process_group_info(world, dt_rank, args.steps, local, dev)
 
     # per-kernel roofline from the live events: forward launches vs backward launches
     kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}
@@ -276,17 +407,19 @@ def main():
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
+            "process_group": pg,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(n, train=train)
             if args.graph == "ER":
-                out["cpu_baseline_env_step"] = cpu_env_step_baseline(n)
+                out["cpu_baseline"] = cpu_refcost_baseline(n)
+                out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+            out["cpu_baseline_learn_loop"] = cpu_baseline(n, train=train)
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()
 
 
-def inference_bench(args, world, rank, dev, dist):
+def inference_bench(args, world, rank, local, dev, dist):
     """configs[4] (gset) / configs[1] (er20): batched greedy rollouts, one vector step = MPNN forward +
     fused greedy argmax (dqn.py:490-512 via experiments/utils.py:154-187) + env step for every episode."""
     from eco_hip import _lib
@@ -336,7 +469,9 @@ def inference_bench(args, world, rank, dev, dist):
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    dt = max_over_ranks(time.perf_counter() - t0, device=dev)
+    dt_rank = time.perf_counter() - t0
+    dt = max_over_ranks(dt_rank, device=dev)
+    pg = process_group_info(world, dt_rank, args.steps, local, dev)
     net.timer = None
     fwd_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timers) / max(len(timers), 1)
     nnz = int(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
@@ -365,13 +500,14 @@ def inference_bench(args, world, rank, dev, dist):
                          "frac": fl / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                          "avg_launch_ms": fwd_ms, "flops_per_launch": fl},
             "best_cut_after_steps": best_cut,
+            "process_group": pg,
         }
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()
 
 
-def envstep_bench(args, world, rank, dev, dist):
+def envstep_bench(args, world, rank, local, dev, dist):
     """SURVEY.md 8d sub-bench: the batched env step kernel alone (spinsystem.py:355-559 for the chosen
     scorer), random actions drawn beforehand, B episodes of ER(n, 0.15).  HBM-bound: algorithmic bytes per
     env-step = state read + write (spins 1, neighbour sum 4, time-since-flip 2 B per vertex, best spins read)
@@ -412,7 +548,9 @@ def envstep_bench(args, world, rank, dev, dist):
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    dt = max_over_ranks(time.perf_counter() - t0, device=dev)
+    dt_rank = time.perf_counter() - t0
+    dt = max_over_ranks(dt_rank, device=dev)
+    pg = process_group_info(world, dt_rank, steps, local, dev)
     env.check_errors()
     k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
     nnz = float(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
@@ -433,6 +571,7 @@ def envstep_bench(args, world, rank, dev, dist):
             "roofline": {"bound": "hbm", "kernel": "env_step", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "avg_launch_ms": k_ms, "bytes_per_launch": per_step},
+            "process_group": pg,
         }
         print(json.dumps(out))
     if dist:
@@ -440,4 +579,4 @@ def envstep_bench(args, world, rank, dev, dist):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -52,6 +52,15 @@ __global__ void er_scan_kernel(int first, int count, int N, const int32_t* row_c
   const int g = first + gi;
   int32_t* rp = row_ptr + (size_t)g * (N + 1);
   const int32_t* rc = row_cnt + (size_t)gi * N;
+  int total = 0;
+  for (int i = lane; i < N; i += 64) total += rc[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+  if (total > cap) {  // overflow: leave an empty graph (valid = 0 after prepare) and report it
+    for (int i = lane; i <= N; i += 64) rp[i] = 0;
+    if (lane == 0) atomicCAS(err, 0, ECO_ERR_GRAPH);
+    return;
+  }
   int base = 0;
   if (lane == 0) rp[0] = 0;
   for (int i0 = 0; i0 < N; i0 += 64) {
@@ -66,7 +75,6 @@ __global__ void er_scan_kernel(int first, int count, int N, const int32_t* row_c
     if (i < N) rp[i + 1] = base + v;
     base += __shfl(v, 63, 64);
   }
-  if (lane == 0 && base > cap) atomicCAS(err, 0, ECO_ERR_GRAPH);
 }
 
 // pass 3: fill sorted columns (wave per row)
@@ -140,18 +148,21 @@ __global__ void ba_kernel(int first, int count, int N, int m, uint64_t seed, int
   }
   __syncthreads();
   int32_t* rp = row_ptr + (size_t)g * (N + 1);
+  __shared__ int overflow;
   if (lane == 0) {
     int s = 0;
-    rp[0] = 0;
     for (int i = 0; i < N; ++i) {
       cur[i] = s;
       s += deg[i];
-      rp[i + 1] = s;
     }
-    if (s > cap) atomicCAS(err, 0, ECO_ERR_GRAPH);
+    overflow = s > cap;
+    if (overflow) atomicCAS(err, 0, ECO_ERR_GRAPH);
   }
   __syncthreads();
-  if (rp[N] > cap) return;
+  for (int i = lane; i <= N; i += 64)  // overflow: an empty graph (valid = 0 after prepare)
+    rp[i] = overflow ? 0 : (i == 0 ? 0 : cur[i - 1] + deg[i - 1]);
+  if (overflow) return;
+  __syncthreads();
   uint32_t* ed = edges + edge_base[g];
   if (lane == 0) {  // deterministic fill order
     for (int e = 0; e < E; ++e) {

@@ -292,7 +292,9 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
       const int oi = __shfl_xor(besti, o, 64);
       if (oq > bestq || (oq == bestq && oi < besti)) { bestq = oq; besti = oi; }
     }
-    int action = besti;
+    // no allowed vertex (irreversible episode with every spin flipped): the reference's
+    // masked_fill(-10000).argmax over an all-masked row returns index 0 (dqn.py:416-428, :505-511)
+    int action = besti == 0x7fffffff ? 0 : besti;
     const uint64_t r0 = rng3(a.act.seed, a.act.counter, (uint64_t)e);
     if (u01(r0) < a.act.epsilon && n_allowed > 0) {  // random.uniform(0,1) >= eps -> greedy
       const uint64_t r1 = rng3(a.act.seed ^ 0xA5A5A5A5ull, a.act.counter, (uint64_t)e);

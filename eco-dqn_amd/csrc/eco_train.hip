@@ -337,10 +337,13 @@ __global__ void td_kernel(const float* q_s, const float* q_tn, const int32_t* a_
                           float* dq, float* sqerr) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  float qt = q_tn[(size_t)b * N + a_star[b]];
+  int as = a_star[b];
+  if ((unsigned)as >= (unsigned)N) as = 0;  // never index outside the row (all-masked argmax is 0)
+  float qt = q_tn[(size_t)b * N + as];
   if (clip && qt < 0.f) qt = 0.f;  // clip_Q_targets (dqn.py:431-432)
   const float td = rewards[b] + (1.f - dones[b]) * gamma * qt;
-  const int a = actions[b];
+  int a = actions[b];
+  if ((unsigned)a >= (unsigned)N) a = 0;
   const float q = q_s[(size_t)b * N + a];
   const float diff = q - td;
   dq[(size_t)b * N + a] = 2.f * diff / (float)B;  // mse_loss(reduction='mean') backward

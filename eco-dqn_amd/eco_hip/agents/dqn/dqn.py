@@ -110,15 +110,13 @@ class DQN:
                                else np.asarray(graph_pool_ids))
         # Fresh graphs per episode like the reference's generators (utils.py:165-236): the store
         # holds 2B slots, episode batch k runs on half k % 2 while the other half is regenerated on
-        # the device.  Replay entries reference graph ids, so the ring must not outlive one episode
-        # batch: capacity <= B * max_steps.
+        # the device.  Replay entries reference graph ids, so a half is only regenerated once every
+        # entry pushed while it was in use has been overwritten (_switch_graph_half).
         self.regenerate_graphs = regenerate_graphs
         self._pool_half = 0
         if regenerate_graphs is not None:
             if self.graphs.n_graphs < 2 * envs.n_envs or not hasattr(self.graphs, "cap"):
                 raise ValueError("regenerate_graphs needs GraphStore.slots(2 * n_envs, ...)")
-            if replay_buffer_size > envs.n_envs * envs.max_steps:
-                raise ValueError("replay_buffer_size must be <= n_envs * max_steps when regenerating graphs")
         self._rng = np.random.default_rng(self.seed)
 
         self.evaluate = evaluate
@@ -226,99 +224,258 @@ class DQN:
                                      _lib.stream_ptr()))
         net.repack()
         self.grad_steps += 1
-        self._samples_since_sync += m
+        self._samples_since_sync += m * self.world
         return self.loss_dev.item() if sync_loss else self.loss_dev.clone()
 
     def sync_target(self):
         """dqn.py:346-347: target <- online."""
         self.target_network.flat.copy_(self.network.flat)
 
-    def _new_graph_ids(self, n):
+    def _switch_graph_half(self, n):
+        """Graph ids for a full reset.  With regenerate_graphs the store holds two halves of B
+        slots: the next batch runs on the other half, regenerated on the device first -- unless a
+        replay entry may still reference it (fewer than `capacity` pushes since that half was last
+        in use, e.g. episodes shorter than max_steps), in which case its graphs are reused."""
         if self.regenerate_graphs is not None:
             kind, param = self.regenerate_graphs[:2]
             weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
-            half = self._pool_half
-            self._pool_half ^= 1
-            self.graphs.generate(half * self.B, self.B, kind, param,
-                                 seed=int(self._rng.integers(1 << 62)), weights=weights)
+            self._half_last_push[self._pool_half] = self._pushed
+            half = self._pool_half ^ 1
+            self._pool_half = half
+            if self._pushed - self._half_last_push[half] >= self.replay_buffer_size:
+                self.graphs.generate(half * self.B, self.B, kind, param,
+                                     seed=int(self._rng.integers(1 << 62)), weights=weights)
             return half * self.B + np.arange(n)
         return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
 
+    def _random_graph_ids(self, n):
+        """Graph ids for episodes reset on their own (an episode that ended before the others):
+        random graphs of the active half (regenerate_graphs) or of the pool."""
+        if self.regenerate_graphs is not None:
+            return self._pool_half * self.B + self._rng.integers(0, self.B, n)
+        return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
+
     def vector_step(self, is_training_ready):
-        """One act -> env.step -> replay.add over all B episodes; returns the new obs buffer."""
+        """One act -> env.step -> replay.add over all B episodes; returns the new obs buffer.
+        Every episode is live here: finished ones are reset by iteration() right after the step
+        that ended them (the reference resets on done, dqn.py:306-327)."""
         x = self.env.obs_x
         nxt = self._obs[1] if x.data_ptr() == self._obs[0].data_ptr() else self._obs[0]
         self.act(x, self.env.graph_ids, is_training_ready, actions_out=self._actions)
         _, rew, done = self.env.step(self._actions, obs_out=nxt)
         self.replay_buffer.add_batch(x, nxt, self.env.graph_ids, self._actions, rew, done)
+        self._pushed += self.B
         return nxt
 
     def start(self):
         """Reset every episode on fresh pool graphs (start of learn)."""
-        self.env.reset(graph_ids=self._new_graph_ids(self.B), seed=self.seed)
+        self._pushed = 0
+        self._half_last_push = [-(1 << 62), -(1 << 62)]
+        self.env.reset(graph_ids=self._switch_graph_half(self.B), seed=self.seed)
         self._steps_in_episode = 0
         self._timestep = 0
         self._ready = False
         self._k_per_vec = max(1, int(round(self.B * self.replay_ratio / self.M)))
         self._last_loss = None
+        self._loss_log = []
+        # every episode ends exactly at max_steps only for reversible spins with Stopping.NORMAL
+        # (spinsystem.py:539-554); otherwise dones are read back after each vector step
+        self._lockstep = self.env.reversible_spins and self.env.cfg.stopping == 1
 
     def iteration(self):
         """One vector step of DQN.learn (dqn.py:273-347): act/step/add for all B episodes, reset
-        finished episodes, then K gradient steps (replay ratio preserved) with target syncs."""
+        finished episodes, then K gradient steps (replay ratio preserved) with target syncs.
+        Schedules count global env-steps: B per rank per vector step, times the world size."""
         B, T = self.B, self.env.max_steps
         if not self._ready and len(self.replay_buffer) >= max(self.replay_start_size, self.M):
             self._ready = True
         self.vector_step(self._ready)
-        self._timestep += B
+        self._timestep += B * self.world
         self._steps_in_episode += 1
         if self.update_exploration:
             self.update_epsilon(self._timestep)
         if self.update_learning_rate:
             self.update_lr(self._timestep)
-        if self._steps_in_episode == T:  # every episode shares T and started together
-            self.env.reset(graph_ids=self._new_graph_ids(B), seed=self.seed + self._timestep)
-            self._steps_in_episode = 0
+        if self._lockstep:
+            if self._steps_in_episode == T:
+                self.env.reset(graph_ids=self._switch_graph_half(B), seed=self.seed + self._timestep)
+                self._steps_in_episode = 0
+        else:
+            done = self.env.dones.bool()
+            n_done = int(done.sum())
+            if n_done == B:
+                self.env.reset(graph_ids=self._switch_graph_half(B), seed=self.seed + self._timestep)
+                self._steps_in_episode = 0
+            elif n_done:
+                self.env.reset(graph_ids=self._random_graph_ids(B), mask=done, seed=self.seed + self._timestep)
         if self._ready:
+            step_losses = []
             for _ in range(self._k_per_vec):
                 self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False)
+                step_losses.append(self._last_loss)
                 if self._samples_since_sync >= self.target_sync_samples:
                     self.sync_target()
                     self._samples_since_sync = 0.0
+            self._loss_log.append((self._timestep, torch.cat(step_losses)))
         return self._last_loss
 
     def learn(self, timesteps, verbose=False, on_vector_step=None):
-        """dqn.py:256-395 with B episodes per vector step (timesteps counts env-steps)."""
+        """dqn.py:256-395 with B episodes per vector step on each rank (timesteps counts global
+        env-steps).  As in the reference, once training is ready: every `test_frequency` env-steps
+        evaluate_agent() and save `<network_save_path>_best` when the score beats every earlier one
+        (:349-364); every `save_network_frequency` env-steps save `<network_save_path><t>` (:366-372);
+        at the end pickle test_scores / losses / solutions (:377-394).  A vector step that crosses
+        k * frequency counts as reaching timestep k * frequency.  Files are written by rank 0.
+        Returns the last 100 (timestep, loss) pairs."""
+        import pickle
         self.start()
-        losses = []
+        rank = torch.distributed.get_rank() if self.dist else 0
+        test_scores, test_solutions = [], []
         while self._timestep < timesteps:
-            loss = self.iteration()
-            if loss is not None:
-                losses.append((self._timestep, loss))
+            t_prev = self._timestep
+            self.iteration()
+            t = self._timestep
             if on_vector_step is not None:
-                on_vector_step(self._timestep)
-        return [(t, float(l.item())) for t, l in losses[-100:]]
+                on_vector_step(t)
+            if not self._ready:
+                continue
+            if self.evaluate and (self.test_envs is not None) and t // self.test_frequency > t_prev // self.test_frequency:
+                tk = (t // self.test_frequency) * self.test_frequency
+                test_score, test_solution = self.evaluate_agent()
+                if verbose and rank == 0:
+                    print('\nTest score: {}\nTest solution: {}\n'.format(np.round(test_score, 3),
+                                                                        np.round(test_solution, 3)))
+                if all(test_score > sc for _, sc in test_scores) and rank == 0:
+                    main, ext = os.path.splitext(self.network_save_path)
+                    self.save(main + "_best" + (ext or ".pth"))
+                test_scores.append([tk, test_score])
+                test_solutions.append([tk, test_solution])
+            if t // self.save_network_frequency > t_prev // self.save_network_frequency and rank == 0:
+                tk = (t // self.save_network_frequency) * self.save_network_frequency
+                main, ext = os.path.splitext(self.network_save_path)
+                self.save(main + str(tk) + (ext or ".pth"))
+        losses = self.losses()
+        if rank == 0 and self.test_save_path is not None:
+            path = self.test_save_path
+            if os.path.splitext(path)[-1] == '':
+                path += '.pkl'
+            folder = os.path.split(self.test_save_path)[0]
+            for p_, arr in ((path, test_scores), (os.path.join(folder, "losses.pkl"), losses),
+                            (os.path.join(folder, "solution.pkl"), test_solutions)):
+                with open(p_, 'wb+') as output:
+                    pickle.dump(np.array(arr), output, pickle.HIGHEST_PROTOCOL)
+                if verbose:
+                    print('saved to {}'.format(p_))
+        self.test_scores, self.test_solutions = test_scores, test_solutions
+        return losses[-100:]
+
+    def losses(self):
+        """[[timestep, loss], ...] of every gradient step so far (dqn.py:339, one host copy)."""
+        out = []
+        for t, l in self._loss_log:
+            for v in l.cpu().tolist():
+                out.append([t, v])
+        return out
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
-    def evaluate_agent(self, test_env=None):
-        """dqn.py:514-602 with TestMetric.BEST: greedy rollouts of every test episode to the end;
-        returns (mean best score, mean best solution)."""
+    def evaluate_agent(self, batch_size=None, test_env=None):
+        """dqn.py:514-602: greedy rollouts of `test_episodes` episodes, at most `batch_size`
+        (default minibatch_size) at a time, on the test VecSpinSystem whose n_envs slots hold the
+        concurrent episodes.  Episodes take the test graphs in order, continuing across calls (the
+        ordered SetGraphGenerator of train_eco.py:69).  A finished episode's slot is refilled before
+        the next prediction, and each prediction couples norm.max() over the active episodes only
+        (predict on obs_batch, :546-547).  test_metric:
+          BEST              -> (best_score, best_solution)  (:564-566)
+          FINAL             -> (score, solution) of the final spins (:567-569)
+          CUMULATIVE_REWARD -> (sum of rewards, 0)          (:560-561, :580-581)
+          ENERGY_ERROR      -> (0, 0), as in the reference whose branch is commented out (:571-583)
+        Returns (mean score, mean solution)."""
         env = test_env or self.test_envs
-        env.reset(graph_ids=np.arange(env.n_envs) % env.graphs.n_graphs, seed=self.seed)
-        gids = env.graph_ids
-        acts = torch.empty(env.n_envs, dtype=torch.int32, device=self.device)
-        for _ in range(env.max_steps):
-            self.network.forward_graphs(env.obs_x, env.graphs, gids, norm_scope=_lib.ECO_NORM_PER_CALL,
-                                        act=self._act_config(0.0), actions_out=acts)
-            env.step(acts)
-        st = env.read()
-        return float(st["best_score"].mean()), float(st["best_solution"].mean())
+        if isinstance(env, (list, tuple)):
+            env = env[0]
+        slots = min(int(batch_size or self.minibatch_size), env.n_envs)
+        dev = self.device
+        if not hasattr(env, "_eval_next_graph"):
+            env._eval_next_graph = 0
+        n_graphs = env.graphs.n_graphs
+        # every slot holds a valid episode (unused ones run to their end and stay masked)
+        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.seed)
+        active = torch.zeros(env.n_envs, dtype=torch.bool, device=dev)
+        cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
+        acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
+        scores, solutions = [], []
+        started = 0
+        metric = self.test_metric
+        act_cfg = self._act_config(0.0)
+        act_cfg.reversible = int(env.reversible_spins)
+        act_cfg.allowed_value = float(env.allowed_action_value())
+        while len(scores) < self.test_episodes:
+            free = (~active[:slots]).nonzero().flatten().cpu().numpy()
+            take = free[:max(0, self.test_episodes - started)]
+            if len(take):
+                mask = np.zeros(env.n_envs, dtype=np.uint8)
+                mask[take] = 1
+                gids = np.zeros(env.n_envs, dtype=np.int64)
+                gids[take] = (env._eval_next_graph + np.arange(len(take))) % n_graphs
+                env._eval_next_graph = (env._eval_next_graph + len(take)) % n_graphs
+                env.reset(graph_ids=gids, mask=mask, seed=self.seed + started)
+                active[torch.as_tensor(take, device=dev)] = True
+                cum[torch.as_tensor(take, device=dev)] = 0.0
+                started += len(take)
+            idx = active.nonzero().flatten()
+            act_cfg.counter = 0
+            if len(idx) == env.n_envs:
+                self.network.forward_graphs(env.obs_x, env.graphs, env.graph_ids, norm_scope=_lib.ECO_NORM_PER_CALL,
+                                            act=act_cfg, actions_out=acts)
+            else:
+                sub = torch.empty(len(idx), dtype=torch.int32, device=dev)
+                self.network.forward_graphs(env.obs_x[idx].contiguous(), env.graphs, env.graph_ids[idx],
+                                            norm_scope=_lib.ECO_NORM_PER_CALL, act=act_cfg, actions_out=sub)
+                acts.zero_()
+                acts[idx] = sub
+            _, rew, done = env.step(acts)
+            cum[active] += rew[active]
+            fin = active & done.bool()
+            if bool(fin.any()):
+                st = env.read()
+                for i in fin.nonzero().flatten().cpu().tolist():
+                    if metric == TestMetric.BEST:
+                        sc, so = float(st["best_score"][i]), float(st["best_solution"][i])
+                    elif metric == TestMetric.FINAL:
+                        sc, so = float(st["score"][i]), self._final_solution(env, st, i)
+                    elif metric == TestMetric.CUMULATIVE_REWARD:
+                        sc, so = float(cum[i]), 0.0
+                    else:
+                        sc, so = 0.0, 0.0
+                    scores.append(sc)
+                    solutions.append(so)
+                active &= ~fin
+        if metric == TestMetric.ENERGY_ERROR:
+            print("\n{}/{} graphs solved optimally".format(np.count_nonzero(np.array(scores) == 0),
+                                                          self.test_episodes), end="")
+        return float(np.mean(scores)), float(np.mean(solutions))
+
+    @staticmethod
+    def _final_solution(env, st, i):
+        """scorer.get_solution of the episode's current spins (score_solver.py:263-271, 377-381,
+        463-467, 537-544, 649-656, 776-783) from the env's integer state."""
+        t = env.cfg.optimisation_target
+        score, lb, qn = float(st["score"][i]), float(st["lower_bound"][i]), float(st["quality_normalizer"][i])
+        invalid = float(st["invalidity"][i]) != 0
+        size = float(st["set_size"][i])
+        if t == _lib.ECO_TARGET_CUT:
+            return score - abs(min(0.0, lb))
+        if t == _lib.ECO_TARGET_MIN_CUT:
+            return max(0.0, qn) - score
+        if t in (_lib.ECO_TARGET_MIN_COVER, _lib.ECO_TARGET_MIN_DOM_SET):
+            return float(env.n_spins) if invalid else size
+        return 0.0 if invalid else size
 
     # ------------------------------------------------------------ checkpoint
     def save(self, path='network.pth'):
-        """dqn.py:604-607: torch.save(state_dict) -- loadable by the reference MPNN."""
-        if os.path.splitext(path)[-1] == '':
-            path = path + '.pth'
+        """dqn.py:604-607: torch.save(state_dict) -- loadable by the reference MPNN.  The reference's
+        extension fix-up is a no-op expression (`path + '.pth'`, :606), so `path` is used as given."""
         torch.save({k: v.detach().cpu().clone() for k, v in self.network.state_dict().items()}, path)
 
     def load(self, path):

@@ -185,8 +185,9 @@ class GraphStore:
         st.generate(0, n_graphs, kind, param, seed, weights)
         return st
 
-    def generate(self, first, count, kind, param, seed, weights="discrete", stream=None):
-        """Regenerate graphs [first, first+count) in place on the device (eco_graphs_generate)."""
+    def generate(self, first, count, kind, param, seed, weights="discrete", stream=None, check=True):
+        """Regenerate graphs [first, first+count) in place on the device (eco_graphs_generate);
+        check=True synchronises and raises on an edge-slot overflow."""
         if not hasattr(self, "cap"):
             raise ValueError("generate() needs a store created with GraphStore.slots()")
         ws = torch.empty(_lib.lib.eco_graphs_generate_workspace_bytes(self.n_spins, count), dtype=torch.uint8,
@@ -195,6 +196,12 @@ class GraphStore:
         _lib.check(_lib.lib.eco_graphs_generate(ctypes.byref(self.gs), first, count, k, float(param),
                                                 int(weights == "discrete"), ctypes.c_uint64(seed), self.cap,
                                                 _lib.ptr(ws), _lib.stream_ptr(stream)))
+        if check:  # an edge-slot overflow leaves an empty graph and sets the device error word
+            self.check_errors(stream)
+
+    def check_errors(self, stream=None):
+        """Synchronise `stream` and raise the first device-side error (eco_check_errors)."""
+        _lib.check(_lib.lib.eco_check_errors(_lib.stream_ptr(stream)))
 
     @classmethod
     def from_dense(cls, matrices, device="cuda"):

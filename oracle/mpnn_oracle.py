@@ -34,11 +34,16 @@ SHAPES = [(64, 7), (63, 8), (64, 64)] + [(64, 128)] * 6 + [(64, 64), (1, 128), (
 N_PARAMS = sum(int(torch.tensor(s).prod()) for s in SHAPES)   # 58,425
 
 
-def init_weights(gen, std=0.01):
+def shapes(n_obs_in=7):
+    """Parameter shapes of MPNN(n_obs_in) in state_dict order (mpnn.py:20-23, :86-87, :111-112, :129-139)."""
+    return [(64, n_obs_in), (63, n_obs_in + 1)] + SHAPES[2:]
+
+
+def init_weights(gen, std=0.01, n_obs_in=7):
     """dqn.py:199-205: Linear weights ~ normal(0, std); the readout bias keeps its
     nn.Linear default U(-1/sqrt(128), 1/sqrt(128))."""
     w = {}
-    for k, s in zip(KEYS, SHAPES):
+    for k, s in zip(KEYS, shapes(n_obs_in)):
         if k.endswith("bias"):
             w[k] = (torch.rand(s, generator=gen) * 2 - 1) / (128 ** 0.5)
         else:
@@ -46,8 +51,10 @@ def init_weights(gen, std=0.01):
     return w
 
 
-def forward(w, obs, n_obs_in=7):
-    """MPNN.forward on obs [B, n_obs_in+N, N] (or [n_obs_in+N, N]) -> Q [B, N] (squeezed like :75)."""
+def forward(w, obs, n_obs_in=7, norm_max=None):
+    """MPNN.forward on obs [B, n_obs_in+N, N] (or [n_obs_in+N, N]) -> Q [B, N] (squeezed like :75).
+    norm_max: the `norm.max()` of mpnn.py:102, taken over the whole input tensor; pass the value of a
+    larger batch explicitly to evaluate that batch in chunks (a chunk's own max would differ)."""
     if obs.dim() == 2:
         obs = obs.unsqueeze(0)
     obs = obs.transpose(-1, -2)                                       # :44 (copy, not in place)
@@ -65,7 +72,9 @@ def forward(w, obs, n_obs_in=7):
     ef = ef * (adj.unsqueeze(-1) != 0).float()
     emb = F.relu(ef.reshape(B, N * N, -1) @ w[KEYS[1]].T).reshape(B, N, N, -1)
     emb = emb.sum(dim=2) / norm
-    e = F.relu(torch.cat([emb, norm / norm.max()], dim=-1) @ w[KEYS[2]].T)
+    nmax = norm.max() if norm_max is None else torch.as_tensor(float(norm_max), dtype=norm.dtype,
+                                                                    device=norm.device)
+    e = F.relu(torch.cat([emb, norm / nmax], dim=-1) @ w[KEYS[2]].T)
     for i in range(3):                                                # :68-72, :114-120
         agg = torch.matmul(adj, h) / norm
         m = F.relu(torch.cat([agg, e], dim=-1) @ w[KEYS[3 + 2 * i]].T)
@@ -79,22 +88,36 @@ def forward(w, obs, n_obs_in=7):
 
 
 def train_step(w, adam_state, states, actions, rewards, states_next, dones,
-               gamma=0.95, lr=1e-4, eps=1e-8, target_w=None, double_dqn=True):
-    """dqn.py:403-451 for a reversible env (gather/argmax over all N actions).
-    `adam_state` = dict(step=int, m={k: tensor}, v={k: tensor}); torch.optim.Adam
-    semantics (bias-corrected, eps added to sqrt(v_hat)).  Returns (new_w, loss)."""
+               gamma=0.95, lr=1e-4, eps=1e-8, target_w=None, double_dqn=True, n_obs_in=7,
+               reversible=True, allowed_value=-1.0):
+    """dqn.py:403-451.  Reversible env: gather/argmax over all N actions (:408-415).  Irreversible
+    (S2V) env: actions whose spin row differs from the allowed action state are masked to -10000
+    before the argmax / max (:417-428); a terminal s' (every action masked) gives argmax 0, and its
+    (1 - done) factor zeroes the term.  `adam_state` = dict(step=int, m={k: tensor}, v={k: tensor});
+    torch.optim.Adam semantics (bias-corrected, eps added to sqrt(v_hat)).  Returns (new_w, loss)."""
     target_w = w if target_w is None else target_w
+    B = states_next.shape[0]
     with torch.no_grad():
-        if double_dqn:
-            a_star = forward(w, states_next).reshape(states_next.shape[0], -1).argmax(1, True)
-            q_t = forward(target_w, states_next).reshape(states_next.shape[0], -1).gather(1, a_star)
+        if reversible:
+            if double_dqn:
+                a_star = forward(w, states_next, n_obs_in).reshape(B, -1).argmax(1, True)
+                q_t = forward(target_w, states_next, n_obs_in).reshape(B, -1).gather(1, a_star)
+            else:
+                q_t = forward(target_w, states_next, n_obs_in).reshape(B, -1).max(1, True)[0]
         else:
-            q_t = forward(target_w, states_next).reshape(states_next.shape[0], -1).max(1, True)[0]
+            target_preds = forward(target_w, states_next, n_obs_in).reshape(B, -1)
+            disallowed = states_next[:, 0, :] != allowed_value
+            if double_dqn:
+                preds = forward(w, states_next, n_obs_in).reshape(B, -1).masked_fill(disallowed, -10000)
+                q_t = target_preds.gather(1, preds.argmax(1, True))
+            else:
+                q_t = target_preds.masked_fill(disallowed, -10000).max(1, True)[0]
     td = rewards + (1 - dones) * gamma * q_t
     wg = {k: v.clone().requires_grad_(True) for k, v in w.items()}
-    q = forward(wg, states).reshape(states.shape[0], -1).gather(1, actions)
+    q = forward(wg, states, n_obs_in).reshape(states.shape[0], -1).gather(1, actions)
     loss = F.mse_loss(q, td, reduction="mean")
     loss.backward()
+    adam_state["grad"] = {k: wg[k].grad.detach().clone() for k in KEYS}  # loss.backward() result
     adam_state["step"] += 1
     t = adam_state["step"]
     new_w = {}

@@ -282,6 +282,95 @@ def make_dqn_step():
     np.savez_compressed(os.path.join(HERE, "dqn_step.npz"), **out)
 
 
+def make_dqn_step_s2v():
+    """Three DQN.train_step calls on IRREVERSIBLE (S2V) ER-20 transitions: the -10000 masking of
+    disallowed actions before the double-DQN argmax (dqn.py:414-428), including terminal next
+    states where every spin is flipped (all actions masked: argmax 0, (1 - done) zeroes the term)."""
+    rng = np.random.default_rng(1999)
+    n, M = 20, 16
+    J = graphs.er_graph(n, 0.15, rng)
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), n, **env_args("s2v", n))
+    net_fn = lambda: MPNN(n_obs_in=1, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)  # noqa: E731
+    agent = DQN([env], net_fn, init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
+                replay_start_size=10, replay_buffer_size=100, gamma=0.95, update_target_frequency=1000,
+                update_learning_rate=False, initial_learning_rate=1e-4, peak_learning_rate=1e-4,
+                final_learning_rate=1e-4, update_frequency=32, minibatch_size=M, max_grad_norm=None,
+                weight_decay=0, update_exploration=True, initial_exploration_rate=1,
+                final_exploration_rate=0.05, final_exploration_step=150000, adam_epsilon=1e-8,
+                logging=False, loss="mse", save_network_frequency=10**9, network_save_path="/tmp/n.pth",
+                evaluate=False, test_envs=None, test_episodes=1, test_frequency=10**9,
+                test_save_path="/tmp/ts.pkl", seed=6)
+    with torch.no_grad():
+        for p in agent.target_network.parameters():
+            p.add_(torch.randn_like(p) * 0.01)
+    out = {"allowed_action_state": np.float64(agent.allowed_action_state)}
+    for k, v in state_dict_np(agent.network).items():
+        out["w0/" + k] = v
+    for k, v in state_dict_np(agent.target_network).items():
+        out["target/" + k] = v
+    steps = 3
+    for s in range(steps):
+        sts, acts, rews, nxt, dns = [], [], [], [], []
+        for i in range(M):
+            Jg = graphs.er_graph(n, 0.15, rng)
+            e = ising_env.make("SpinSystem", SingleGraphGenerator(Jg), n, **env_args("s2v", n))
+            o = e.reset()
+            order = rng.permutation(n)
+            # every 4th transition is the episode's last flip (terminal s')
+            k = n - 1 if i % 4 == 0 else int(rng.integers(0, n - 1))
+            for a in order[:k]:
+                o, _, _, _ = e.step(int(a))
+            a = int(order[k])
+            o2, r, d, _ = e.step(a)
+            sts.append(o); acts.append([a]); rews.append([r]); nxt.append(o2); dns.append([float(d)])
+        tr = [torch.as_tensor(np.array(sts)), torch.as_tensor(np.array(acts), dtype=torch.long),
+              torch.as_tensor(np.array(rews), dtype=torch.float), torch.as_tensor(np.array(nxt)),
+              torch.as_tensor(np.array(dns), dtype=torch.float)]
+        out[f"s{s}/states"] = np.array(sts)
+        out[f"s{s}/actions"] = np.array(acts)
+        out[f"s{s}/rewards"] = np.array(rews, dtype=np.float32)
+        out[f"s{s}/states_next"] = np.array(nxt)
+        out[f"s{s}/dones"] = np.array(dns, dtype=np.float32)
+        loss = agent.train_step(tr)
+        out[f"s{s}/loss"] = np.float64(loss)
+        for k2, v in state_dict_np(agent.network).items():
+            out[f"s{s}/w/" + k2] = v
+    out["steps"] = np.int64(steps)
+    np.savez_compressed(os.path.join(HERE, "dqn_step_s2v.npz"), **out)
+
+
+def make_schedules():
+    """DQN.update_epsilon / update_lr (dqn.py:467-488) over a range of timesteps for two
+    hyper-parameter sets (train_eco.py:136-146 and a warm-up/decay learning-rate schedule)."""
+    n = 20
+    J = graphs.er_graph(n, 0.15, np.random.default_rng(5))
+    env = ising_env.make("SpinSystem", SingleGraphGenerator(J), 2 * n, **env_args("eco", n))
+    net_fn = lambda: MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)  # noqa: E731
+    sets = [dict(initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
+                 initial_learning_rate=1e-4, peak_learning_rate=1e-4, peak_learning_rate_step=20000,
+                 final_learning_rate=1e-4, final_learning_rate_step=200000),
+            dict(initial_exploration_rate=0.9, final_exploration_rate=0.1, final_exploration_step=12345,
+                 initial_learning_rate=0, peak_learning_rate=1e-3, peak_learning_rate_step=10000,
+                 final_learning_rate=5e-5, final_learning_rate_step=200000)]
+    ts = np.array([0, 1, 7, 999, 5000, 10000, 10001, 12345, 12346, 20000, 100000, 199999, 200000, 200001,
+                   799999, 800000, 10 ** 7], dtype=np.int64)
+    out = {"timesteps": ts}
+    for i, hp in enumerate(sets):
+        agent = DQN([env], net_fn, replay_start_size=10, replay_buffer_size=100, logging=False,
+                    evaluate=False, seed=1, network_save_path="/tmp/n.pth", test_save_path="/tmp/ts.pkl", **hp)
+        eps, lrs = [], []
+        for t in ts:
+            agent.update_epsilon(int(t))
+            agent.update_lr(int(t))
+            eps.append(agent.epsilon)
+            lrs.append(agent.optimizer.param_groups[0]["lr"])
+        out[f"h{i}/eps"] = np.array(eps, dtype=np.float64)
+        out[f"h{i}/lr"] = np.array(lrs, dtype=np.float64)
+        for k, v in hp.items():
+            out[f"h{i}/{k}"] = np.float64(v)
+    np.savez_compressed(os.path.join(HERE, "schedules.npz"), **out)
+
+
 def make_greedy_rollout():
     """Pretrained-net greedy rollout (dqn.py:490-512 predict) on one ER-200 graph:
     actions plus the top-1/top-2 Q margin per step (argmax-tie robustness)."""
@@ -446,7 +535,8 @@ def make_env_problems():
 if __name__ == "__main__":
     random.seed(0)
     np.random.seed(0)
-    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "greedy_rollout", "greedy_solver",
+    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "dqn_step_s2v", "schedules",
+                              "greedy_rollout", "greedy_solver",
                               "env_problems"]
     for w in which:
         globals()["make_" + w]()

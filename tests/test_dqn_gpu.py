@@ -10,22 +10,24 @@ import pytest
 import torch
 
 from conftest import GOLDEN
+from oracle import graphs as og
 from oracle import mpnn_oracle as mo
+from oracle import spinsystem_oracle as so
 
 pytestmark = pytest.mark.gpu
 
 
 def _split(obs, n_obs=7):
     obs = np.asarray(obs)
-    x = np.zeros((obs.shape[0], obs.shape[2], 8), np.float32)
+    x = np.zeros((obs.shape[0], obs.shape[2], 8 if n_obs <= 8 else 16), np.float32)
     x[:, :, :n_obs] = obs[:, :n_obs, :].transpose(0, 2, 1).astype(np.float32)
     return torch.from_numpy(x).cuda(), [a for a in obs[:, n_obs:, :]]
 
 
-def _flat_to_dict(flat):
+def _flat_to_dict(flat, n_obs=7):
     from eco_hip.networks.mpnn import param_layout
     out, off = {}, 0
-    for name, shape in param_layout(7):
+    for name, shape in param_layout(n_obs):
         n = int(np.prod(shape))
         out[name] = flat[off:off + n].reshape(shape)
         off += n
@@ -85,7 +87,7 @@ def _dqn_for(store, n, B=16, **kw):
                 replay_buffer_size=4096, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
                 initial_learning_rate=1e-4, peak_learning_rate=1e-4, final_learning_rate=1e-4,
                 update_frequency=32, minibatch_size=64, final_exploration_rate=0.05, final_exploration_step=150000,
-                adam_epsilon=1e-8, seed=3)
+                adam_epsilon=1e-8, seed=3, evaluate=False, test_save_path=None)
     args.update(kw)
     return DQN(env, lambda: MPNN(device="cuda"), **args)
 
@@ -161,3 +163,184 @@ def test_learn_short_run_updates_and_is_finite():
     # target sync happened at least once and tracks the online net exactly when it does
     agent.sync_target()
     assert torch.equal(agent.target_network.flat, agent.network.flat)
+
+
+def _s2v_env(store, n, B, T=None):
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (Observable, RewardSignal, ExtraAction, OptimisationTarget, SpinBasis)
+    # experiments/train_eco.py:311-315 S2V settings
+    return VecSpinSystem(store, B, T or n, observables=[Observable.SPIN_STATE], reward_signal=RewardSignal.DENSE,
+                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                         spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=None,
+                         reversible_spins=False)
+
+
+def _s2v_dqn(env, **kw):
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN
+    args = dict(init_weight_std=0.01, double_dqn=True, clip_Q_targets=False, replay_start_size=64,
+                replay_buffer_size=4096, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
+                initial_learning_rate=1e-4, peak_learning_rate=1e-4, final_learning_rate=1e-4,
+                update_frequency=32, minibatch_size=64, final_exploration_rate=0.05, final_exploration_step=150000,
+                adam_epsilon=1e-8, seed=4, evaluate=False, test_save_path=None)
+    args.update(kw)
+    return DQN(env, lambda: MPNN(n_obs_in=1, device="cuda"), **args)
+
+
+def test_train_step_s2v_matches_reference_three_steps():
+    """Irreversible (S2V) train_step (dqn.py:414-428): disallowed actions masked before the double-DQN
+    argmax, terminal next states (every spin flipped: all masked, argmax 0) included -- against three
+    consecutive reference train steps (tests/golden/dqn_step_s2v.npz).  Bars as the ECO test."""
+    f = np.load(os.path.join(GOLDEN, "dqn_step_s2v.npz"))
+    from eco_hip.graphs import GraphStore
+    n, M = 20, 16
+    states = [f[f"s{s}/states"] for s in range(int(f["steps"]))]
+    adj = [a for st in states for a in st[:, 1:, :]]
+    store = GraphStore.from_dense(adj)
+    agent = _s2v_dqn(_s2v_env(store, n, M), minibatch_size=M)
+    assert agent.allowed_value == float(f["allowed_action_state"])
+    agent.network.load_state_dict({k: torch.from_numpy(f["w0/" + k]) for k in mo.KEYS})
+    agent.target_network.load_state_dict({k: torch.from_numpy(f["target/" + k]) for k in mo.KEYS})
+    for s in range(int(f["steps"])):
+        p = f"s{s}/"
+        xs, _ = _split(f[p + "states"], 1)
+        xn, _ = _split(f[p + "states_next"], 1)
+        gid = torch.arange(s * M, (s + 1) * M, dtype=torch.int32, device="cuda")
+        act = torch.from_numpy(f[p + "actions"][:, 0].astype(np.int32)).cuda()
+        rew = torch.from_numpy(f[p + "rewards"][:, 0]).cuda()
+        done = torch.from_numpy(f[p + "dones"][:, 0]).cuda()
+        loss = agent.train_step((xs, act, rew, xn, done, gid))
+        ref_loss = float(f[p + "loss"])
+        assert np.isfinite(loss)
+        assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss)), (s, loss, ref_loss)
+        # terminal s' has no allowed action: the fused argmax returns 0 like masked_fill(-1e4).argmax
+        term = f[p + "dones"][:, 0] == 1
+        assert (agent.a_star.cpu().numpy()[term] == 0).all()
+        got = _flat_to_dict(agent.network.flat.cpu(), 1)
+        for k in mo.KEYS:
+            np.testing.assert_allclose(got[k].numpy(), f[p + "w/" + k], rtol=0, atol=2e-6, err_msg=f"step {s} {k}")
+
+
+def test_learn_s2v_resets_finished_episodes():
+    """S2V episodes end after N flips, before max_steps = 2N: iteration() resets them at once, so no
+    dead steps are pushed (every stored transition comes from a live episode: exactly one terminal per
+    episode) and every episode restarts from all -1 spins."""
+    from eco_hip.graphs import GraphStore
+    n, B = 20, 64
+    store = GraphStore.random("ER", 256, n, 0.15, seed=9)
+    env = _s2v_env(store, n, B, T=2 * n)
+    agent = _s2v_dqn(env, replay_buffer_size=B * 2 * n * 4, replay_start_size=B * 3 * n)
+    agent.start()
+    for _ in range(3 * n):
+        agent.iteration()
+    assert agent.grad_steps > 0
+    rb = agent.replay_buffer
+    size = len(rb)
+    assert size == B * 3 * n
+    dones = rb.done[:size].cpu().numpy().reshape(3 * n, B)
+    # episodes of exactly n steps, back to back: terminal at vector steps n-1, 2n-1, 3n-1
+    expect = np.zeros(3 * n)
+    expect[[n - 1, 2 * n - 1, 3 * n - 1]] = 1
+    np.testing.assert_array_equal(dones, np.repeat(expect[:, None], B, axis=1))
+    # s of the first step of each episode is all -1 (irreversible reset, spinsystem.py:295-297)
+    xs = rb.xs[:size].cpu().numpy().reshape(3 * n, B, n, 8)
+    for t0 in (0, n, 2 * n):
+        assert (xs[t0, :, :, 0] == -1).all()
+    assert np.isfinite(agent.losses()).all()
+
+
+def _oracle_greedy_chunk(w, mats, inits, T, metric_rows):
+    """Lockstep greedy rollouts of one evaluate_agent batch: predict couples norm.max() over the
+    active batch (dqn.py:546-547).  Returns per episode (best_score, best_solution, final score,
+    final cut, cumulative reward, tie flag)."""
+    envs = [so.SpinSystemOracle(J, T, basin_reward=1. / J.shape[0]) for J in mats]
+    obs = [e.reset(spins=s) for e, s in zip(envs, inits)]
+    cum = [0.0] * len(envs)
+    tie = False
+    for _ in range(T):
+        q = mo.forward(w, torch.from_numpy(np.array(obs)).float()).reshape(len(envs), -1)
+        top = torch.topk(q, 2, dim=1).values
+        tie = tie or bool((top[:, 0] - top[:, 1] < 1e-4).any())
+        acts = q.argmax(1)
+        for i, e in enumerate(envs):
+            obs[i], r, _, _ = e.step(int(acts[i]))
+            cum[i] += r
+    return [(e.best_score, e.best_solution, e.score, so.calculate_cut(e.state[0], e.matrix), c, tie)
+            for e, c in zip(envs, cum)]
+
+
+@pytest.mark.parametrize("metric", ["BEST", "FINAL", "CUMULATIVE_REWARD", "ENERGY_ERROR"])
+def test_evaluate_agent_matches_oracle(metric):
+    """evaluate_agent (dqn.py:514-602): 6 test episodes in batches of 4 (a refill batch of 2 couples
+    norm.max() over 2 graphs), graphs taken in order, greedy MPNN rollouts vs the oracle's."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.agents.dqn.utils import TestMetric
+    n, T = 20, 40
+    rng = np.random.default_rng(31)
+    mats = [og.er_graph(n, 0.3, rng) for _ in range(6)]
+    store = GraphStore.from_dense(mats)
+    kw = dict(observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS, extra_action=ExtraAction.NONE,
+              optimisation_target=OptimisationTarget.CUT, spin_basis=SpinBasis.SIGNED, norm_rewards=True,
+              basin_reward=1. / n)
+    test_env = VecSpinSystem(store, 4, T, **kw)
+    agent = _dqn_for(GraphStore.random("ER", 8, n, 0.15, seed=1), n, B=8, test_envs=test_env, test_episodes=6,
+                     minibatch_size=4, test_metric=TestMetric[metric])
+    w = mo.init_weights(torch.Generator().manual_seed(8), std=0.1)
+    agent.network.load_state_dict(w)
+    score, sol = agent.evaluate_agent()
+    # the initial spins evaluate_agent drew: the same masked resets on a twin env
+    twin = VecSpinSystem(store, 4, T, **kw)
+    inits = []
+    for seed, gids in ((agent.seed, [0, 1, 2, 3]), (agent.seed + 4, [4, 5])):
+        mask = np.zeros(4, np.uint8)
+        mask[:len(gids)] = 1
+        twin.reset(graph_ids=np.array(gids + [0] * (4 - len(gids))), mask=mask, seed=seed)
+        sp = twin.read(spins=True)["spins"].cpu().numpy()
+        inits.append(sp[:len(gids)].astype(np.int64))
+    res = (_oracle_greedy_chunk(w, mats[:4], inits[0], T, None) + _oracle_greedy_chunk(w, mats[4:], inits[1], T, None))
+    if any(r[5] for r in res):
+        pytest.skip("near-tie in the oracle rollout")
+    col = {"BEST": (0, 1), "FINAL": (2, 3), "CUMULATIVE_REWARD": (4, None), "ENERGY_ERROR": (None, None)}[metric]
+    exp_s = np.mean([r[col[0]] for r in res]) if col[0] is not None else 0.0
+    exp_o = np.mean([r[col[1]] for r in res]) if col[1] is not None else 0.0
+    assert score == pytest.approx(exp_s, rel=1e-12, abs=1e-12)
+    assert sol == pytest.approx(exp_o, rel=1e-12, abs=1e-12)
+    # the next call continues with the following graphs in order (ordered SetGraphGenerator)
+    assert test_env._eval_next_graph == 0
+
+
+def test_learn_evaluates_saves_and_pickles(tmp_path):
+    """learn() side effects (dqn.py:349-394): evaluate every test_frequency env-steps once training
+    is ready, `_best` network on a new best, periodic checkpoints, and the three pickles."""
+    import pickle
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.agents.dqn.utils import TestMetric
+    n, B = 20, 64
+    store = GraphStore.random("ER", 256, n, 0.15, seed=4)
+    test_env = VecSpinSystem(GraphStore.random("ER", 8, n, 0.15, seed=5), 8, 2 * n,
+                             **{k: v for k, v in _dqn_for(store, n, B=B).env.env_args.items()})
+    net_path = str(tmp_path / "network.pth")
+    agent = _dqn_for(store, n, B=B, replay_start_size=2 * B, train_minibatch=64, evaluate=True,
+                     test_envs=test_env, test_episodes=8, test_frequency=B * 10, test_metric=TestMetric.BEST,
+                     save_network_frequency=B * 20, network_save_path=net_path,
+                     test_save_path=str(tmp_path / "test_scores.pkl"))
+    agent.learn(timesteps=B * 41)
+    with open(tmp_path / "test_scores.pkl", "rb") as fh:
+        ts = pickle.load(fh)
+    assert [int(t) for t in ts[:, 0]] == [B * 10, B * 20, B * 30, B * 40]
+    assert (tmp_path / "network_best.pth").exists()
+    for k in (20, 40):
+        assert (tmp_path / f"network{B * k}.pth").exists()
+    with open(tmp_path / "losses.pkl", "rb") as fh:
+        lo = pickle.load(fh)
+    assert lo.shape[1] == 2 and len(lo) == agent.grad_steps and np.isfinite(lo).all()
+    with open(tmp_path / "solution.pkl", "rb") as fh:
+        sol = pickle.load(fh)
+    assert sol.shape == (4, 2)
+    # the saved checkpoint is a plain state_dict with the reference's keys
+    sd = torch.load(tmp_path / f"network{B * 40}.pth", map_location="cpu", weights_only=True)
+    assert list(sd) == mo.KEYS

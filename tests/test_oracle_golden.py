@@ -9,6 +9,7 @@ import torch
 from conftest import GOLDEN
 from oracle import spinsystem_oracle as so
 from oracle import mpnn_oracle as mo
+from oracle import graphs as og
 
 
 def _digest(a):
@@ -128,3 +129,41 @@ def test_greedy_solver_matches_reference():
         acts = so.greedy_solve(env)
         np.testing.assert_array_equal(acts, f[p + "actions"])
         assert env.best_solution == f[p + "best_solution"]
+
+
+def test_oracle_train_step_s2v_matches_reference():
+    """Irreversible (S2V) train_step: -10000 masking before the double-DQN argmax (dqn.py:414-428),
+    terminal next states included (tests/golden/dqn_step_s2v.npz)."""
+    f = np.load(os.path.join(GOLDEN, "dqn_step_s2v.npz"))
+    w = _weights(f, "w0/")
+    tw = _weights(f, "target/")
+    st = {"step": 0, "m": {}, "v": {}}
+    assert f["s0/dones"].sum() >= 3
+    for s in range(int(f["steps"])):
+        p = f"s{s}/"
+        w, loss = mo.train_step(
+            w, st, torch.from_numpy(f[p + "states"]).float(), torch.from_numpy(f[p + "actions"]),
+            torch.from_numpy(f[p + "rewards"]), torch.from_numpy(f[p + "states_next"]).float(),
+            torch.from_numpy(f[p + "dones"]), target_w=tw, n_obs_in=1, reversible=False,
+            allowed_value=float(f["allowed_action_state"]))
+        assert abs(loss - float(f[p + "loss"])) <= 1e-6 * max(1.0, abs(float(f[p + "loss"])))
+        for k in mo.KEYS:
+            np.testing.assert_allclose(w[k].numpy(), f[p + "w/" + k], rtol=1e-5, atol=1e-7)
+
+
+def test_oracle_norm_max_chunking():
+    """forward(norm_max=) evaluates a batch in chunks exactly as one call (mpnn.py:102 batch coupling)."""
+    g = torch.Generator().manual_seed(5)
+    w = mo.init_weights(g, std=0.1)
+    rng = np.random.default_rng(3)
+    obs = []
+    for n_edges_p in (0.1, 0.3, 0.5, 0.2):
+        J = og.er_graph(16, n_edges_p, rng)
+        x = rng.random((7, 16))
+        obs.append(np.vstack([x, J]))
+    obs = torch.from_numpy(np.array(obs)).float()
+    full = mo.forward(w, obs)
+    nmax = float(((obs[:, 7:, :] != 0).sum(1)).clamp(min=1).max())
+    parts = torch.cat([mo.forward(w, obs[i:i + 1], norm_max=nmax).reshape(1, -1) for i in range(4)])
+    torch.testing.assert_close(parts, full, rtol=0, atol=1e-6)
+    assert not torch.allclose(mo.forward(w, obs[0]), full[0], atol=1e-6)  # the coupling is real
