@@ -339,7 +339,7 @@ class DQN:
                 on_vector_step(t)
             if not self._ready:
                 continue
-            if self.evaluate and (self.test_envs is not None) and t // self.test_frequency > t_prev // self.test_frequency:
+            if self.evaluate and t // self.test_frequency > t_prev // self.test_frequency:
                 tk = (t // self.test_frequency) * self.test_frequency
                 test_score, test_solution = self.evaluate_agent()
                 if verbose and rank == 0:
@@ -392,6 +392,12 @@ class DQN:
           ENERGY_ERROR      -> (0, 0), as in the reference whose branch is commented out (:571-583)
         Returns (mean score, mean solution)."""
         env = test_env or self.test_envs
+        if env is None:
+            # dqn.py:225-227: test on the training environment(s) -- here a separate batch of episodes
+            # over the training graph pool (the training episodes keep running untouched)
+            from ...envs.batched import VecSpinSystem
+            env = self.test_envs = VecSpinSystem(self.graphs, max(1, int(batch_size or self.minibatch_size)),
+                                                 self.env.max_steps, **self.env.env_args)
         if isinstance(env, (list, tuple)):
             env = env[0]
         slots = min(int(batch_size or self.minibatch_size), env.n_envs)
@@ -454,6 +460,7 @@ class DQN:
         if metric == TestMetric.ENERGY_ERROR:
             print("\n{}/{} graphs solved optimally".format(np.count_nonzero(np.array(scores) == 0),
                                                           self.test_episodes), end="")
+        self.last_evaluation = (scores, solutions)  # per episode, in completion order
         return float(np.mean(scores)), float(np.mean(solutions))
 
     @staticmethod

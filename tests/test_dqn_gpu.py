@@ -229,7 +229,7 @@ def test_learn_s2v_resets_finished_episodes():
     n, B = 20, 64
     store = GraphStore.random("ER", 256, n, 0.15, seed=9)
     env = _s2v_env(store, n, B, T=2 * n)
-    agent = _s2v_dqn(env, replay_buffer_size=B * 2 * n * 4, replay_start_size=B * 3 * n)
+    agent = _s2v_dqn(env, replay_buffer_size=B * 2 * n * 4, replay_start_size=B * n)
     agent.start()
     for _ in range(3 * n):
         agent.iteration()
@@ -256,17 +256,17 @@ def _oracle_greedy_chunk(w, mats, inits, T, metric_rows):
     envs = [so.SpinSystemOracle(J, T, basin_reward=1. / J.shape[0]) for J in mats]
     obs = [e.reset(spins=s) for e, s in zip(envs, inits)]
     cum = [0.0] * len(envs)
-    tie = False
+    tie = np.zeros(len(envs), bool)   # per episode: its own argmax only depends on its own state
     for _ in range(T):
         q = mo.forward(w, torch.from_numpy(np.array(obs)).float()).reshape(len(envs), -1)
         top = torch.topk(q, 2, dim=1).values
-        tie = tie or bool((top[:, 0] - top[:, 1] < 1e-4).any())
+        tie |= (top[:, 0] - top[:, 1] < 1e-4 * (1 + top[:, 0].abs())).numpy()
         acts = q.argmax(1)
         for i, e in enumerate(envs):
             obs[i], r, _, _ = e.step(int(acts[i]))
             cum[i] += r
-    return [(e.best_score, e.best_solution, e.score, so.calculate_cut(e.state[0], e.matrix), c, tie)
-            for e, c in zip(envs, cum)]
+    return [(e.best_score, e.best_solution, e.score, so.calculate_cut(e.state[0], e.matrix), c, bool(t))
+            for e, c, t in zip(envs, cum, tie)]
 
 
 @pytest.mark.parametrize("metric", ["BEST", "FINAL", "CUMULATIVE_REWARD", "ENERGY_ERROR"])
@@ -288,7 +288,7 @@ def test_evaluate_agent_matches_oracle(metric):
     test_env = VecSpinSystem(store, 4, T, **kw)
     agent = _dqn_for(GraphStore.random("ER", 8, n, 0.15, seed=1), n, B=8, test_envs=test_env, test_episodes=6,
                      minibatch_size=4, test_metric=TestMetric[metric])
-    w = mo.init_weights(torch.Generator().manual_seed(8), std=0.1)
+    w = mo.init_weights(torch.Generator().manual_seed(8), std=0.5)  # well-separated Q (no argmax near-ties)
     agent.network.load_state_dict(w)
     score, sol = agent.evaluate_agent()
     # the initial spins evaluate_agent drew: the same masked resets on a twin env
@@ -301,13 +301,20 @@ def test_evaluate_agent_matches_oracle(metric):
         sp = twin.read(spins=True)["spins"].cpu().numpy()
         inits.append(sp[:len(gids)].astype(np.int64))
     res = (_oracle_greedy_chunk(w, mats[:4], inits[0], T, None) + _oracle_greedy_chunk(w, mats[4:], inits[1], T, None))
-    if any(r[5] for r in res):
-        pytest.skip("near-tie in the oracle rollout")
     col = {"BEST": (0, 1), "FINAL": (2, 3), "CUMULATIVE_REWARD": (4, None), "ENERGY_ERROR": (None, None)}[metric]
-    exp_s = np.mean([r[col[0]] for r in res]) if col[0] is not None else 0.0
-    exp_o = np.mean([r[col[1]] for r in res]) if col[1] is not None else 0.0
-    assert score == pytest.approx(exp_s, rel=1e-12, abs=1e-12)
-    assert sol == pytest.approx(exp_o, rel=1e-12, abs=1e-12)
+    got_s, got_o = agent.last_evaluation
+    # episodes complete in lockstep: batch 1 in slot order, then batch 2
+    assert len(got_s) == 6
+    checked = 0
+    for i, r in enumerate(res):
+        if r[5]:
+            continue   # a near-tie argmax in the oracle rollout: trajectories may legitimately differ
+        checked += 1
+        assert got_s[i] == (r[col[0]] if col[0] is not None else 0.0), (i, got_s[i], r)
+        assert got_o[i] == (r[col[1]] if col[1] is not None else 0.0), (i, got_o[i], r)
+    assert checked >= 3, "too many near-ties to check the rollouts"
+    if checked == 6:
+        assert score == pytest.approx(np.mean(got_s), rel=1e-15) and sol == pytest.approx(np.mean(got_o), rel=1e-15)
     # the next call continues with the following graphs in order (ordered SetGraphGenerator)
     assert test_env._eval_next_graph == 0
 
