@@ -41,6 +41,7 @@ __device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
 
 }  // namespace eco
 #include "eco_mpnn_dense.h"  // dense-aggregation kernels (after the phase-timing buffer)
+#include "eco_mpnn_shared.h"  // many episodes on one shared large graph (G22)
 namespace eco {
 
 __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
@@ -1000,8 +1001,12 @@ extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packe
 
 extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
   if (n_spins < 1 || batch < 1) return 0;
-  if (n_spins > MPNN_MAX_SPINS)  // + per episode Z/h ping-pong rows and e rows (mpnn_forward_large_kernel)
-    return 256 + (size_t)batch * ((n_spins + 15) & ~15) * 64 * 3 * sizeof(float);
+  if (n_spins > MPNN_MAX_SPINS) {  // + per episode Z/h ping-pong rows and e rows (mpnn_forward_large_kernel),
+                                  // or the node-major buffers of the shared-graph path, whichever is larger
+    const size_t per_ep = (size_t)batch * ((n_spins + 15) & ~15) * 64 * 3 * sizeof(float);
+    const size_t shared = shared_ws_bytes(n_spins, batch);
+    return 256 + (per_ep > shared ? per_ep : shared);
+  }
   return 256;  // the call-scope norm.max() slot
 }
 
@@ -1093,6 +1098,9 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     return mpnn_forward_dense_launch(a, saved != nullptr, st);
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
+    // one graph shared by every episode (GSet best-cut search): node-major episode-batched kernels
+    static const bool no_shared = getenv("ECO_MPNN_NO_SHARED") != nullptr;  // A/B knob
+    if (gs->n_graphs == 1 && gs->unit_weights && !no_shared) return mpnn_forward_shared_launch(a, workspace, st);
     const int rows_pad = (N + 15) & ~15;
     const size_t lds = (size_t)readout_scratch_floats(rows_pad, 1, 8, true) * sizeof(float);
     (void)hipFuncSetAttribute((const void*)mpnn_forward_large_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,

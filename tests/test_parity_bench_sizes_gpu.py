@@ -210,3 +210,52 @@ def test_large_forward_n2000_matches_oracle(episodes):
                        act=ActConfig(0.0, 1, 0.0, 1, 0), actions_out=acts)
     assert torch.equal(acts.long(), qc.argmax(1))
     torch.testing.assert_close(qc, q, rtol=0, atol=0)  # one graph: per-call max == per-graph max
+
+
+@pytest.mark.parametrize("weights", ["uniform", "discrete"])
+def test_shared_graph_forward_matches_per_episode_and_oracle(weights):
+    """The node-major shared-graph path (one graph, many episodes: eco_mpnn_shared.h) against the
+    per-episode large kernel on the same graph replicated per episode, and against the oracle for a few
+    episodes; 37 episodes = two full 16-episode slices + a padded one; +-1 weights exercise A- (V rows).
+    Fused greedy act, and irreversible epsilon-greedy act restricted to allowed vertices."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ActConfig, ECO_NORM_PER_CALL
+    n, B = 600, 37
+    rng = np.random.default_rng(600)
+    J = og.er_graph(n, 0.02, rng, weights=weights)
+    one = GraphStore.from_dense([J])
+    rep = GraphStore.from_dense([J] * B)
+    g = torch.Generator().manual_seed(6)
+    w = mo.init_weights(g, std=0.1)
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    q1 = net.forward_graphs(xc, one, torch.zeros(B, dtype=torch.int32, device="cuda"), norm_scope=ECO_NORM_PER_CALL)
+    qr = net.forward_graphs(xc, rep, torch.arange(B, dtype=torch.int32, device="cuda"), norm_scope=ECO_NORM_PER_CALL)
+    err = float(((q1 - qr).abs() / (1 + qr.abs())).max())
+    assert err <= 5e-5, err
+    wc = {k: v.cuda() for k, v in w.items()}
+    adj = torch.from_numpy(J).float().cuda().unsqueeze(0)
+    for b in (0, 15, 16, 36):
+        with torch.no_grad():
+            ref = mo.forward(wc, _obs(xc[b:b + 1], adj))
+        assert float(((q1[b] - ref).abs() / (1 + ref.abs())).max()) <= 5e-5, b
+    gz = torch.zeros(B, dtype=torch.int32, device="cuda")
+    acts = torch.empty(B, dtype=torch.int32, device="cuda")
+    qa = torch.empty(B, n, device="cuda")
+    net.forward_graphs(xc, one, gz, norm_scope=ECO_NORM_PER_CALL, q_out=qa, act=ActConfig(0.0, 1, 0.0, 1, 0),
+                       actions_out=acts)
+    assert torch.equal(acts.long(), qa.argmax(1))
+    # irreversible: only vertices whose feature 0 == -1 may be chosen (greedy and random)
+    for eps in (0.0, 1.0):
+        net.forward_graphs(xc, one, gz, norm_scope=ECO_NORM_PER_CALL, act=ActConfig(eps, 0, -1.0, 3, 1),
+                           actions_out=acts)
+        a = acts.long().cpu()
+        assert bool((x[torch.arange(B), a, 0] == -1).all())
+        if eps == 0.0:
+            masked = qa.cpu().masked_fill(x[:, :, 0] != -1, float("-inf"))
+            assert torch.equal(a, masked.argmax(1))
