@@ -3,13 +3,16 @@
 //
 // The per-episode large kernel (mpnn_forward_large_kernel) gathers a 256-B embedding row per edge per
 // episode from that episode's private rows: 4 x nnz x 256 B per episode, ~41 GB per 1024-episode call,
-// served by HBM.  Here every buffer is NODE-major, [node][episode][64] fp32, so one wave tile = one node
-// x 16 episodes (the 16 rows of the MFMA node operand) and one neighbour's contribution to the tile is
-// one contiguous 4-KB row block.  The aggregation A.[H_1 ... H_B] reads each neighbour block once per
-// 16 episodes, and the episode slices are dealt so that all workgroups of one group (one per XCD: block
-// b works for group b % 8) sweep the nodes of the same 16-episode slice together: the slice's H
-// (N x 4 KB = 8 MB at G22) is what the gathers of that XCD re-read, from L2 / the Infinity Cache, while
-// HBM sees each H row written once and read about once per layer.
+// served by HBM.  Here every buffer is NODE-major, [node][episode][64] fp32, so the rows of one node for a
+// slice of consecutive episodes are one contiguous block, and one neighbour's contribution to a wave tile
+// is one such block per tile node.  The aggregation A.[H_1 ... H_B] then reads each neighbour block once per
+// slice of 4 episodes, and the slices are dealt so that all workgroups of one group (one per XCD: block b
+// works for group b % 8) sweep the nodes of the same slice together: the slice's H (N x 1 KB = 2 MB at
+// G22) is what the gathers of that XCD re-read, from its 4-MB L2.  A wave tile is 4 nodes of similar
+// degree (visited by decreasing degree) x the slice's 4 episodes = the 16 rows of the MFMA node operand;
+// the tiles' CSR rows are pre-interleaved into one padded edge table per call, so the 4 nodes walk their
+// rows in lockstep without per-lane bounds.  (16-episode slices of one node: 8 MB per slice, 28 % L2 hits,
+// ~8 GB fetched per layer at 6 TB/s.)
 //
 // Phases (one launch each, the layer weights staged in LDS by LDS-DMA once per persistent workgroup):
 //   prep:    U = relu(Wx.x + w_a), V = relu(Wx.x - w_a) and h0 = relu(W0.x) per node and episode
@@ -26,20 +29,26 @@
 
 namespace eco {
 
-constexpr int SH_EPS = 16;     // episodes per wave tile
-constexpr int SH_NW = 8;       // waves per workgroup
-constexpr int SH_GROUPS = 8;   // episode-slice groups: one per XCD (block b -> group b % 8)
-constexpr int SH_TILE = SH_EPS * 64;  // floats of one node's 16-episode row block
+constexpr int SH_EPS = 4;              // episodes per slice
+constexpr int SH_NPT = 16 / SH_EPS;    // nodes per wave tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
+constexpr int SH_NW = 16;              // waves per workgroup (one workgroup per CU: <= 128 VGPRs)
+constexpr int SH_GROUPS = 8;           // episode-slice groups: one per XCD (block b -> group b % 8)
+constexpr int SH_PART = SH_EPS * 64;   // floats of one slice's column-sum partial
 
 struct SharedBufs {
-  float* U;     // [N][Epad][64]
-  float* V;
+  float* U;       // [N + 1][4][Epad][16] (node, feature chunk, episode, 16 features): row N is the zero row the
+                  // padded edge-table slots point at
+  float* V;       // (graphs with negative weights only)
   float* HA;
   float* HB;
-  float* EB;
-  float* part;  // [S][nlb][16][64] column-sum partials of h3
-  float* ql;    // [Epad][N] Wr[64:] . h3
-  int Epad, S, nlb;
+  float* EB;      // [N][4][Epad][16]
+  float* part;    // [S][ntiles][SH_EPS][64] column-sum partials of h3, one per wave tile
+  float* ql;      // [Epad][N] Wr[64:] . h3
+  int32_t* perm;  // [N] nodes by decreasing degree
+  int32_t* tinfo; // [ntiles][SH_NPT] {node} , [ntiles][SH_NPT] {norm}, [ntiles] {max row length}
+  uint32_t* et;   // [ntiles][MD][SH_NPT] interleaved edge words (edge q of tile node k at q * SH_NPT + k)
+  int32_t* ctr;   // [3 launches][SH_GROUPS] work counters (zeroed per forward)
+  int Epad, S, nlb, ntiles, MD;
 };
 
 inline int shared_grid() {  // persistent workgroups: one per CU, a multiple of the group count
@@ -53,10 +62,14 @@ inline int shared_grid() {  // persistent workgroups: one per CU, a multiple of 
   return g;
 }
 
+// MD: row slots per tile in the edge table = N (the largest possible degree of a simple graph): the
+// table is sized without a device -> host read of max_deg.
 inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
-  const size_t nlb = shared_grid() / SH_GROUPS;
-  return (5 * (size_t)N * Epad * 64 + S * nlb * SH_TILE + Epad * (size_t)N) * sizeof(float);
+  const size_t nlb = shared_grid() / SH_GROUPS, nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
+  (void)nlb;
+  return (4 * ((size_t)N + 1) * Epad * 64 + (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N +
+          nt * (2 * SH_NPT + 1) + nt * (size_t)N * SH_NPT + 4 * SH_GROUPS) * sizeof(float);
 }
 
 inline SharedBufs shared_carve(float* base, int N, int B) {
@@ -64,15 +77,33 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.S = (B + SH_EPS - 1) / SH_EPS;
   sb.Epad = sb.S * SH_EPS;
   sb.nlb = shared_grid() / SH_GROUPS;
-  const size_t T = (size_t)N * sb.Epad * 64;
+  sb.ntiles = (N + SH_NPT - 1) / SH_NPT;
+  sb.MD = N;
+  const size_t T1 = ((size_t)N + 1) * sb.Epad * 64;
   sb.U = base;
-  sb.V = sb.U + T;
-  sb.HA = sb.V + T;
-  sb.HB = sb.HA + T;
-  sb.EB = sb.HB + T;
-  sb.part = sb.EB + T;
-  sb.ql = sb.part + (size_t)sb.S * sb.nlb * SH_TILE;
+  sb.V = sb.U + T1;
+  sb.HA = sb.V + T1;
+  sb.HB = sb.HA + T1;
+  sb.EB = sb.HB + T1;
+  sb.part = sb.EB + (size_t)N * sb.Epad * 64;
+  sb.ql = sb.part + (size_t)sb.S * sb.ntiles * SH_PART;
+  sb.perm = reinterpret_cast<int32_t*>(sb.ql + (size_t)sb.Epad * N);
+  sb.tinfo = sb.perm + N;
+  sb.et = reinterpret_cast<uint32_t*>(sb.tinfo + (size_t)sb.ntiles * (2 * SH_NPT + 1));
+  sb.ctr = reinterpret_cast<int32_t*>(sb.et + (size_t)sb.ntiles * sb.MD * SH_NPT);
   return sb;
+}
+
+// streaming (non-temporal) row access: the layer's own e rows and its output rows are touched once, and
+// should not push the gathered slice of H out of the L2
+__device__ __forceinline__ float4 f4_nt(const float* p) {
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st4_nt(float* p, float4 x) {
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4{x.x, x.y, x.z, x.w}, reinterpret_cast<v4*>(p));
 }
 
 // mm_bf3 over LDS fragments with one output tile's fragments in flight at a time (the shared-graph layer
@@ -99,127 +130,197 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
   }
 }
 
-// U, V, h0 rows: thread (episode row er, feature quad q) of node blockIdx.x, episodes 16 blockIdx.y ..
-// (16 threads write one 256-B row).  Same arithmetic as the phase-A / phase-C expressions of the dense
-// kernel; rows of padding episodes are zero.
+// perm[rank] = node, nodes ranked by decreasing degree (index on ties): one thread per node
+__global__ __launch_bounds__(256) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
+  const int N = a.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int32_t* rp = a.gs.row_ptr + (size_t)a.gids[0] * (N + 1);
+  if (i >= N) return;
+  const int di = rp[i + 1] - rp[i];
+  int r = 0;
+  for (int j = 0; j < N; ++j) {
+    const int dj = rp[j + 1] - rp[j];
+    r += (dj > di) || (dj == di && j < i);
+  }
+  sb.perm[r] = i;
+}
+
+// tile tables: thread (tile t, slot k) -> node, norm, its edge words interleaved with the tile's other
+// nodes (padding slots: column N = the zero row, weight 0), and the tile's longest row
+__global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
+  const int N = a.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int t = i / SH_NPT, k = i % SH_NPT;
+  if (t >= sb.ntiles) return;
+  const int gid = a.gids[0];
+  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
+  const uint32_t* eg = a.gs.edges + a.gs.edge_base[gid];
+  const int slot = t * SH_NPT + k;
+  const bool valid = slot < N;
+  const int n = valid ? sb.perm[slot] : 0;
+  const int len = valid ? rp[n + 1] - rp[n] : 0;
+  sb.tinfo[t * SH_NPT + k] = valid ? n : 0;
+  sb.tinfo[(size_t)sb.ntiles * SH_NPT + t * SH_NPT + k] = valid ? max(a.gs.deg[(size_t)gid * N + n], 1) : 1;
+  int ml = len;
+  for (int o = 1; o < SH_NPT; o <<= 1) ml = max(ml, __shfl_xor(ml, o, 64));  // the tile's 4 slots are lanes 4t'..
+  uint32_t* et = sb.et + (size_t)t * sb.MD * SH_NPT;
+  const int ml4 = (ml + 3) & ~3;
+  for (int q = 0; q < ml4; ++q) et[q * SH_NPT + k] = q < len ? eg[rp[n] + q] : (uint32_t)N;  // pad: col N, w 0
+  if (k == 0) sb.tinfo[(size_t)sb.ntiles * 2 * SH_NPT + t] = ml4;
+}
+
+// U (, V) and h0 for a block of 16 nodes x 16 episodes: the x rows are staged in LDS from 16 contiguous
+// 512-B runs (one per episode), each thread computes one (node, episode) row into an LDS image laid out
+// like the buffers, and the block stores every (node, chunk) run of 16 episodes (1 KB) with consecutive
+// lanes on consecutive 16 B.  Weights staged in LDS.  Same arithmetic as the phase-A / phase-C expressions
+// of the dense kernel; rows of padding episodes and the sentinel node N are zero.  V only for graphs with
+// negative weights (lower bound < 0).
 __global__ __launch_bounds__(256) void shared_prep_kernel(MpnnArgs a, SharedBufs sb) {
-  const int n = blockIdx.x;
-  const int er = threadIdx.x >> 4, q = threadIdx.x & 15;
-  const int e = blockIdx.y * SH_EPS + er;
-  if (e >= sb.Epad) return;
-  const bool valid = e < a.B;
-  float4 xa = zero4(), xb = zero4();
-  if (valid) {
-    xa = f4(a.x + ((size_t)e * a.N + n) * 8);
-    xb = f4(a.x + ((size_t)e * a.N + n) * 8 + 4);
+  __shared__ float WS[1088];                                      // PK_W0 [64][8] | PK_WX [64][8] | PK_WA [64]
+  __shared__ __attribute__((aligned(16))) float XS[16][16][8];     // [episode][node][8]
+  __shared__ __attribute__((aligned(16))) float RB[16][4][16][20]; // [node][chunk][episode][16 (+4 pad)]
+  const int t = threadIdx.x;
+  const int n0 = blockIdx.x * 16, e0 = blockIdx.y * 16;
+  const int N = a.N;
+  for (int i = t; i < 1088; i += 256) WS[i] = a.P[i];
+  {
+    const int el = t >> 4, nl = t & 15;
+    const int e = e0 + el, n = n0 + nl;
+    const bool ok = e < a.B && n < N;
+    float4* xd = reinterpret_cast<float4*>(&XS[el][nl][0]);
+    xd[0] = ok ? f4(a.x + ((size_t)e * N + n) * 8) : zero4();
+    xd[1] = ok ? f4(a.x + ((size_t)e * N + n) * 8 + 4) : zero4();
   }
-  const float* P = a.P;
-  float u[4], v[4], h[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int f = 4 * q + i;
-    const float* wx = P + PK_WX + f * 8;
-    const float z = wx[0] * xa.x + wx[1] * xa.y + wx[2] * xa.z + wx[3] * xa.w + wx[4] * xb.x + wx[5] * xb.y +
-                    wx[6] * xb.z + wx[7] * xb.w;
-    const float* w0 = P + PK_W0 + f * 8;
-    const float h0 = w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
-                     w0[6] * xb.z + w0[7] * xb.w;
-    u[i] = valid ? relu(fmaf(1.f, P[PK_WA + f], z)) : 0.f;
-    v[i] = valid ? relu(fmaf(-1.f, P[PK_WA + f], z)) : 0.f;
-    h[i] = valid ? relu(h0) : 0.f;
+  __syncthreads();
+  const bool neg = a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0;
+  const int nl = t >> 4, el = t & 15;  // compute role: row (node n0 + nl, episode e0 + el)
+  const bool valid = e0 + el < a.B && n0 + nl < N;
+  const float4 xa = *reinterpret_cast<const float4*>(&XS[el][nl][0]);
+  const float4 xb = *reinterpret_cast<const float4*>(&XS[el][nl][4]);
+  const size_t cs = (size_t)sb.Epad * 16;
+  for (int which = 0; which < 3; ++which) {  // 0: U, 1: V, 2: h0
+    if (which == 1 && !neg) continue;
+    float* dst = which == 0 ? sb.U : which == 1 ? sb.V : sb.HA;
+#pragma unroll 4
+    for (int f = 0; f < 64; ++f) {
+      float val;
+      if (which < 2) {
+        const float* wx = WS + PK_WX + f * 8;
+        const float z = wx[0] * xa.x + wx[1] * xa.y + wx[2] * xa.z + wx[3] * xa.w + wx[4] * xb.x + wx[5] * xb.y +
+                        wx[6] * xb.z + wx[7] * xb.w;
+        val = relu(fmaf(which == 0 ? 1.f : -1.f, WS[PK_WA + f], z));
+      } else {
+        const float* w0 = WS + PK_W0 + f * 8;
+        val = relu(w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
+                   w0[6] * xb.z + w0[7] * xb.w);
+      }
+      RB[nl][f >> 4][el][f & 15] = valid ? val : 0.f;
+    }
+    __syncthreads();
+    // 16 nodes x 4 chunks x 16 episodes x 4 float4: thread i -> run (node, chunk), episode, float4
+    for (int i = t; i < 16 * 4 * 16 * 4; i += 256) {
+      const int j4 = i & 3, e_l = (i >> 2) & 15, c = (i >> 6) & 3, n_l = i >> 8;
+      const int n = n0 + n_l;
+      if (n > N) continue;
+      float* o = dst + ((size_t)n * 4 + c) * cs + (size_t)(e0 + e_l) * 16 + 4 * j4;
+      if (e0 + e_l < sb.Epad) st4(o, *reinterpret_cast<const float4*>(&RB[n_l][c][e_l][4 * j4]));
+      if (which == 2 && n == N && e0 + e_l < sb.Epad) st4(sb.HB + ((size_t)n * 4 + c) * cs + (size_t)(e0 + e_l) * 16 + 4 * j4, zero4());
+    }
+    __syncthreads();
   }
-  const size_t o = ((size_t)n * sb.Epad + e) * 64 + 4 * q;
-  st4(sb.U + o, make_float4(u[0], u[1], u[2], u[3]));
-  st4(sb.V + o, make_float4(v[0], v[1], v[2], v[3]));
-  st4(sb.HA + o, make_float4(h[0], h[1], h[2], h[3]));
 }
 
 // PHASE 0: edge embedding -> EB; 1: update layer Hc -> Hn; 2: last update layer -> q_local + column sums.
+// Wave tile: the SH_NPT nodes of tile t (similar degrees) x the slice's SH_EPS episodes; lane row c16 =
+// node kn x episode eps.  The tile's edge table is walked in groups of 4 edges per node, the next group's
+// edge words loaded while the current group's row blocks are in flight; padding slots read the zero row.
 template <int PHASE>
 __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a, SharedBufs sb, int layer,
                                                                      const float* Hc, float* Hn) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   uint16_t* WL = reinterpret_cast<uint16_t*>(lds);  // Wf (24 fragments) or Wm, Wu (96 fragments)
-  float* RED = lds + (96 * BF_FRAG) / 2;            // [SH_NW][16][64] column sums (PHASE 2)
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int c16 = lane & 15, s4 = lane >> 4;
+  const int kn = c16 / SH_EPS, eps = c16 % SH_EPS;
   const uint16_t* PB = reinterpret_cast<const uint16_t*>(a.P + PK_BF);
   if (PHASE == 0) glds_frags<SH_NW>(WL, PB + BF_WF, 24, w, lane);
   else glds_frags<SH_NW>(WL, PB + BF_LAYER + layer * BF_LAYER_STRIDE, 96, w, lane);
   const int N = a.N;
   const int gid = a.gids[0];
-  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
-  const uint32_t* __restrict__ eg = a.gs.edges + a.gs.edge_base[gid];
-  const int32_t* degp = a.gs.deg + (size_t)gid * N;
-  const int grp = blockIdx.x % SH_GROUPS, lb = blockIdx.x / SH_GROUPS;
-  const int nlb = gridDim.x / SH_GROUPS;
+  const int grp = blockIdx.x % SH_GROUPS;  // the XCD's label (round-robin placement; speed only)
+  const int n_slices = (sb.S - grp + SH_GROUPS - 1) / SH_GROUPS;  // slices grp, grp + 8, ...
+  int32_t* ctr = sb.ctr + (PHASE == 0 ? 0 : layer + 1) * SH_GROUPS + grp;
   const float* P = a.P;
   const float md = PHASE == 0 ? (float)(a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : a.gs.max_deg[gid]) : 1.f;
-  const size_t ld = (size_t)sb.Epad * 64;  // floats per node row block of all episodes
+  // [node][chunk c][episode][16]: chunk c of the 4 slice episodes of a node is one 256-B run, so each
+  // gather instruction (fixed c, 16 rows = 4 nodes x 4 episodes) reads 4 whole 256-B runs
+  const size_t ld = (size_t)sb.Epad * 64;  // floats per node block
+  const size_t cs = (size_t)sb.Epad * 16;  // floats per feature chunk of a node block
+  const float* Ub = PHASE == 0 ? sb.U : Hc;
   glds_wait();
   __syncthreads();
-  for (int s = grp; s < sb.S; s += SH_GROUPS) {
-    const int ep = s * SH_EPS + c16;
+  // Work items (slice-major, tile-minor) are taken from the group's counter one tile at a time, so the
+  // waves of one XCD stay within about one slice of each other whatever their speeds (a static split
+  // drifted apart over many slices and the L2 held none of them); the next item is claimed while the
+  // current one is computed.
+  int item = 0;
+  if (lane == 0) item = atomicAdd(ctr, 1);
+  item = __shfl(item, 0, 64);
+  while (true) {
+    const int sl = item / sb.ntiles;
+    if (sl >= n_slices) break;
+    int next = 0;
+    if (lane == 0) next = atomicAdd(ctr, 1);
+    const int s = grp + SH_GROUPS * sl, t = item - sl * sb.ntiles;
+    const int ep = s * SH_EPS + eps;
     const bool evalid = ep < a.B;
-    const size_t co = (size_t)ep * 64 + 4 * s4;  // this lane's offset inside a node row block
-    float4 col[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) col[c] = zero4();
-    for (int n = lb * SH_NW + w; n < N; n += nlb * SH_NW) {
-      const int e0 = rp[n], e1 = rp[n + 1];
-      const float nf = (float)max(degp[n], 1);
+    const size_t co = (size_t)ep * 16 + 4 * s4;  // this lane's offset inside chunk 0 of a node block
+    {
+      const int slot = t * SH_NPT + kn;
+      const bool nvalid = slot < N;
+      const int n = sb.tinfo[t * SH_NPT + kn];
+      const float nf = (float)sb.tinfo[sb.ntiles * SH_NPT + t * SH_NPT + kn];
+      const int ml = uniform_i(sb.tinfo[sb.ntiles * 2 * SH_NPT + t]);
+      const uint32_t* et = sb.et + (size_t)t * sb.MD * SH_NPT + kn;
       float4 acc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[c] = zero4();
-      // gather: 4 neighbours' row blocks in flight, accumulated in CSR order
-      int q = e0;
-      for (; q + 4 <= e1; q += 4) {
-        uint32_t ex[4];
+      uint32_t ex[4], nx[4];
+      if (ml > 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ex[k] = eg[q + k];
+        for (int k = 0; k < 4; ++k) ex[k] = et[k * SH_NPT];
+      }
+      for (int q = 0; q < ml; q += 4) {
+        if (q + 4 < ml) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nx[k] = et[(q + 4 + k) * SH_NPT];  // next group's edge words
+        }
         float4 r[4][4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int wv = edge_w(ex[k]);
-          const float* src = (PHASE == 0 ? (wv > 0 ? sb.U : sb.V) : Hc) + (size_t)edge_col(ex[k]) * ld + co;
+          const float* src = (PHASE == 0 && wv < 0 ? sb.V : Ub) + (size_t)edge_col(ex[k]) * ld + co;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) r[k][c] = f4(src + 16 * c);
+          for (int c = 0; c < 4; ++c) r[k][c] = f4(src + c * cs);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float wv = (float)edge_w(ex[k]);
+          const float fw = PHASE == 0 ? 1.f : (float)edge_w(ex[k]);  // padding: zero row
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (PHASE == 0) {
-              acc[c].x += r[k][c].x; acc[c].y += r[k][c].y; acc[c].z += r[k][c].z; acc[c].w += r[k][c].w;
-            } else {
-              acc[c].x = fmaf(wv, r[k][c].x, acc[c].x); acc[c].y = fmaf(wv, r[k][c].y, acc[c].y);
-              acc[c].z = fmaf(wv, r[k][c].z, acc[c].z); acc[c].w = fmaf(wv, r[k][c].w, acc[c].w);
-            }
+            acc[c].x = fmaf(fw, r[k][c].x, acc[c].x); acc[c].y = fmaf(fw, r[k][c].y, acc[c].y);
+            acc[c].z = fmaf(fw, r[k][c].z, acc[c].z); acc[c].w = fmaf(fw, r[k][c].w, acc[c].w);
           }
         }
-      }
-      for (; q < e1; ++q) {
-        const uint32_t ex = eg[q];
-        const int wv = edge_w(ex);
-        const float* src = (PHASE == 0 ? (wv > 0 ? sb.U : sb.V) : Hc) + (size_t)edge_col(ex) * ld + co;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 rv = f4(src + 16 * c);
-          if (PHASE == 0) {
-            acc[c].x += rv.x; acc[c].y += rv.y; acc[c].z += rv.z; acc[c].w += rv.w;
-          } else {
-            const float fw = (float)wv;
-            acc[c].x = fmaf(fw, rv.x, acc[c].x); acc[c].y = fmaf(fw, rv.y, acc[c].y);
-            acc[c].z = fmaf(fw, rv.z, acc[c].z); acc[c].w = fmaf(fw, rv.w, acc[c].w);
-          }
-        }
+        for (int k = 0; k < 4; ++k) ex[k] = nx[k];
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         acc[c].x = acc[c].x / nf; acc[c].y = acc[c].y / nf; acc[c].z = acc[c].z / nf; acc[c].w = acc[c].w / nf;
       }
+      const bool rvalid = nvalid && evalid;
       const size_t ro = (size_t)n * ld + co;  // this lane's row (node n, episode ep)
       if (PHASE == 0) {
         if (s4 == 3) acc[3].w = nf / md;  // feature 63 = norm / norm.max() (mpnn.py:102)
@@ -227,74 +328,88 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         mm_bf3_seq(d, acc, WL, lane);
+        if (nvalid) {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) st4(sb.EB + ro + 16 * nt, evalid ? relu4(d[nt]) : zero4());
-      } else {
-        float4 ev[4], hc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          ev[c] = f4(sb.EB + ro + 16 * c);
-          hc[c] = f4(Hc + ro + 16 * c);
+          for (int nt = 0; nt < 4; ++nt) st4_nt(sb.EB + ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
         }
+      } else {
         f32x4 d[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         mm_bf3_seq(d, acc, WL, lane);               // message = relu(Wm . [agg, e])
-        mm_bf3_seq(d, ev, WL + BF_HALF, lane);
+        {
+          float4 ev[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ev[c] = f4_nt(sb.EB + ro + c * cs);
+          mm_bf3_seq(d, ev, WL + BF_HALF, lane);
+        }
         float4 mr[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) mr[c] = relu4(d[c]);
         f32x4 hn[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+        {
+          float4 hc[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hc[c] = f4(Hc + ro + c * cs);
+          mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+        }
         mm_bf3_seq(hn, mr, WL + 3 * BF_HALF, lane);
         if (PHASE == 1) {
+          if (nvalid) {
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) st4(Hn + ro + 16 * nt, evalid ? relu4(hn[nt]) : zero4());
+            for (int nt = 0; nt < 4; ++nt) st4_nt(Hn + ro + nt * cs, rvalid ? relu4(hn[nt]) : zero4());
+          }
         } else {
           float qp = 0.f;
+          float* pt = sb.part + ((size_t)s * sb.ntiles + t) * SH_PART + eps * 64 + 4 * s4;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
-            const float4 h3 = evalid ? relu4(hn[nt]) : zero4();
+            const float4 h3 = rvalid ? relu4(hn[nt]) : zero4();
             const int f = 16 * nt + 4 * s4;
             qp = fmaf(h3.x, P[PK_WR + 64 + f], qp);
             qp = fmaf(h3.y, P[PK_WR + 65 + f], qp);
             qp = fmaf(h3.z, P[PK_WR + 66 + f], qp);
             qp = fmaf(h3.w, P[PK_WR + 67 + f], qp);
-            col[nt].x += h3.x; col[nt].y += h3.y; col[nt].z += h3.z; col[nt].w += h3.w;
+            // the tile's column sums over its SH_NPT nodes (fixed butterfly order), one partial per tile
+            float4 csum = h3;
+#pragma unroll
+            for (int o = SH_EPS; o < 16; o <<= 1) {
+              csum.x += __shfl_xor(csum.x, o, 64); csum.y += __shfl_xor(csum.y, o, 64);
+              csum.z += __shfl_xor(csum.z, o, 64); csum.w += __shfl_xor(csum.w, o, 64);
+            }
+            if (kn == 0) st4_nt(pt + 16 * nt, csum);
           }
           qp += __shfl_xor(qp, 16, 64);
           qp += __shfl_xor(qp, 32, 64);
-          if (s4 == 0 && evalid) sb.ql[(size_t)ep * N + n] = qp;
+          if (s4 == 0 && rvalid) sb.ql[(size_t)ep * N + n] = qp;
         }
       }
     }
-    if (PHASE == 2) {  // per-workgroup column sums of this slice, waves combined in a fixed order
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st4(RED + (w * SH_EPS + c16) * 64 + 16 * c + 4 * s4, col[c]);
-      __syncthreads();
-      for (int i = threadIdx.x; i < SH_TILE; i += 64 * SH_NW) {
-        float t = 0.f;
-#pragma unroll
-        for (int k = 0; k < SH_NW; ++k) t += RED[k * SH_TILE + i];
-        sb.part[((size_t)s * nlb + lb) * SH_TILE + i] = t;
-      }
-      __syncthreads();
-    }
+    item = __shfl(next, 0, 64);
   }
 }
 
 // ReadoutLayer (mpnn.py:143-159) + epsilon-greedy act, one wave per episode: column sums from the
 // partials (fixed order), p = Wp . mean, q = relu(p) . Wr[:64] + q_local + b, then the act of readout_act.
-__global__ __launch_bounds__(64) void shared_readout_kernel(MpnnArgs a, SharedBufs sb) {
+__global__ __launch_bounds__(256) void shared_readout_kernel(MpnnArgs a, SharedBufs sb) {
+  __shared__ float red[4][64];
   const int e = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = a.N;
   const float* P = a.P;
   const int s = e / SH_EPS, er = e % SH_EPS;
-  float cs = 0.f;
-  for (int k = 0; k < sb.nlb; ++k) cs += sb.part[((size_t)s * sb.nlb + k) * SH_TILE + er * 64 + lane];
+  {  // the slice's per-tile column sums: wave w takes tiles w, w + 4, ...; the four combined in order
+    const float* pp = sb.part + (size_t)s * sb.ntiles * SH_PART + er * 64 + lane;
+    float c0 = 0.f;
+#pragma unroll 8
+    for (int k = w; k < sb.ntiles; k += 4) c0 += pp[(size_t)k * SH_PART];
+    red[w][lane] = c0;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const float cs = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
   const float mean = cs / (float)N;
   const float* wp = P + PK_WP + lane * 64;
   float p = 0.f;
@@ -361,10 +476,14 @@ __global__ __launch_bounds__(64) void shared_readout_kernel(MpnnArgs a, SharedBu
 
 static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStream_t st) {
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
-  shared_prep_kernel<<<dim3(a.N, sb.S), 256, 0, st>>>(a, sb);
+  shared_perm_kernel<<<(a.N + 255) / 256, 256, 0, st>>>(a, sb);
+  shared_tiles_kernel<<<(sb.ntiles * SH_NPT + 255) / 256, 256, 0, st>>>(a, sb);
+  shared_prep_kernel<<<dim3((a.N + 1 + 15) / 16, (sb.Epad + 15) / 16), 256, 0, st>>>(a, sb);
+  if (hipMemsetAsync(sb.ctr, 0, 4 * SH_GROUPS * sizeof(int32_t), st) != hipSuccess)
+    return fail(ECO_ERR_HIP, "memset failed");
   const int grid = shared_grid();
   const size_t lds_edge = 24 * BF_FRAG * 2, lds_layer = 96 * BF_FRAG * 2,
-               lds_last = lds_layer + (size_t)SH_NW * SH_TILE * sizeof(float);
+               lds_last = lds_layer;
   (void)hipFuncSetAttribute((const void*)shared_layer_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_edge);
   (void)hipFuncSetAttribute((const void*)shared_layer_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -375,7 +494,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   shared_layer_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 0, sb.HA, sb.HB);
   shared_layer_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 1, sb.HB, sb.HA);
   shared_layer_kernel<2><<<grid, 64 * SH_NW, lds_last, st>>>(a, sb, 2, sb.HA, nullptr);
-  shared_readout_kernel<<<a.B, 64, 0, st>>>(a, sb);
+  shared_readout_kernel<<<a.B, 256, 0, st>>>(a, sb);
   return check_launch("mpnn_forward_shared");
 }
 
