@@ -134,6 +134,28 @@ def cpu_refcost_baseline(n=200, seconds=10.0):
 
 
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v4", "pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r02", "train", "pmc_sq_dense.json")
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (~2.5 PF)
+
+
+def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
+    """MFMA evidence of the dominant kernel from the committed SQ PMC pass (profiles/r02/train/
+    pmc_sq_dense.json, ER-200 M=2048): MFMA-busy fraction (launch mix of the train loop: inference forwards
+    of act and of s', training forwards with saved activations) and the ratio of ISSUED bf16 MFMA FLOPs
+    (bf16x3 splits, dense N^2 aggregations) to the algorithmic FLOPs, so the issued rate can be priced
+    against the bf16 peak beside the f32-algorithmic fraction."""
+    if (graph, n, M) != ("ER", 200, 2048) or dom != "mpnn_forward_kernel":
+        return None
+    try:
+        with open(PMC_SQ) as f:
+            k = json.load(f)["kernels"]
+        inf, trn = k["mpnn_forward_dense_kernel<false>"], k["mpnn_forward_dense_kernel<true>"]
+    except (OSError, ValueError, KeyError):
+        return None
+    n_inf, n_trn = 1 + 2 * (B * 2 // M), B * 2 // M  # act + online/target(s') per grad step; online(s) saves
+    busy = (n_inf * inf["mfma_busy"] + n_trn * trn["mfma_busy"]) / (n_inf + n_trn)
+    ratio = inf["issued_bf16_flop"] / (flops_per_graph * M)
+    return {"mfma_busy": busy, "issued_per_algorithmic_flop": ratio, "source": os.path.relpath(PMC_SQ, REPO)}
 
 
 def pmc_traffic(dom, B, M, n, graph="ER"):
@@ -409,6 +431,12 @@ def main():
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
             "process_group": pg,
         }
+        mf = pmc_mfma(dom, B, args.minibatch, n, args.graph, mean_gf) if train else None
+        if mf:
+            issued = achieved * mf["issued_per_algorithmic_flop"]
+            out["roofline"].update(mfma_busy=mf["mfma_busy"], issued_bf16_tflops=issued,
+                                   bf16_peak=BF16_MFMA_PEAK_TFLOPS, bf16_frac=issued / BF16_MFMA_PEAK_TFLOPS,
+                                   mfma_source=mf["source"])
         if not args.no_cpu_baseline and world == 1:
             if args.graph == "ER":
                 out["cpu_baseline"] = cpu_refcost_baseline(n)

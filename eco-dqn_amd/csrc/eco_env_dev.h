@@ -39,6 +39,28 @@ __device__ __forceinline__ void store_obs_row(float* obs_x, size_t row, int nobs
   }
 }
 
+// One observable row value, float64, exactly as spinsystem.py:303-328 / :486-535.
+struct ObsCtx {
+  double mlr, dist_best, hamming, nqi, term, ep_time;
+  int basis;
+};
+// g is passed as the field h; the reference's g = s * (J@s) is a float64 product, so
+// s = -1 with h = +0.0 gives -0.0 (kept: observations are compared bitwise).
+__device__ __forceinline__ double obs_value(int id, const ObsCtx& c, int s, int h, int tsfk, const double* tab) {
+  switch (id) {
+    case ECO_OBS_SPIN_STATE: return c.basis == ECO_BASIS_BINARY ? (double)(1 - s) / 2.0 : (double)s;
+    case ECO_OBS_IMMEDIATE_QUALITY_CHANGE: return ((double)s * (double)h) / c.mlr;
+    case ECO_OBS_TIME_SINCE_FLIP: return tab[tsfk];
+    case ECO_OBS_EPISODE_TIME: return c.ep_time;
+    case ECO_OBS_TERMINATION_IMMANENCY: return c.term;
+    case ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS: return c.nqi;
+    case ECO_OBS_DISTANCE_FROM_BEST_SOLUTION: return c.dist_best;
+    case ECO_OBS_DISTANCE_FROM_BEST_STATE: return c.hamming;
+    case ECO_OBS_VALIDITY_BIT: return 1.0;  // MaxCut: every spin vector is valid
+    default: return 0.0;  // GLOBAL_VALIDITY_DIFFERENCE: (0 - 0) / 1 (the mask observables are rejected)
+  }
+}
+
 // LDS written by a wave and read back by the same wave only: a wave-scope fence suffices
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -5,6 +5,7 @@
 #include <cmath>
 
 #include "eco_mpnn.h"
+#include "eco_env_dev.h"
 
 namespace eco {
 
@@ -451,6 +452,169 @@ __global__ void replay_sample_kernel(eco_replay rb, int size, int M, uint64_t ke
   }
 }
 
+// ------------------------------------------------------------ compact replay ----
+// ReplayBuffer of MaxCut (OptimisationTarget.CUT) transitions as the env's integer state instead of fp32
+// feature rows: per vertex one u32 {spin sign bit 31 | time-since-flip count bits 16..30 | local field
+// h = (J s)_v as int16 bits 0..15} for s and for s', plus per state {|score - best| / mlr, termination
+// immanency, step t, Hamming distance to the best spins} -- 8 B per vertex per transition against 64 B of
+// the feature ring.  The sample kernel rebuilds the fp32 feature rows with the env's own obs_value (the
+// same float64 operations, so the features equal, bit for bit, the rows the env wrote).
+// Ring: rows_s [C][N] u32 | rows_n [C][N] u32 | ctx_s [C][4] f64 | ctx_n [C][4] f64 | gid | act | rew | done
+// [C] | the current state of each env episode: cur_rows [B][N] u32 | cur_ctx [B][4] f64.
+struct CompactRing {
+  uint32_t *rows_s, *rows_n, *cur_rows;
+  double *ctx_s, *ctx_n, *cur_ctx;
+  int32_t *gid, *act;
+  float *rew, *done;
+};
+
+static CompactRing compact_carve(void* base, int N, int C, int B) {
+  CompactRing r;
+  size_t o = 0;
+  char* b = (char*)base;
+  auto take = [&](size_t bytes) { void* p = b + o; o = align_up(o + bytes, 256); return p; };
+  r.rows_s = (uint32_t*)take((size_t)C * N * 4);
+  r.rows_n = (uint32_t*)take((size_t)C * N * 4);
+  r.ctx_s = (double*)take((size_t)C * 4 * 8);
+  r.ctx_n = (double*)take((size_t)C * 4 * 8);
+  r.gid = (int32_t*)take((size_t)C * 4);
+  r.act = (int32_t*)take((size_t)C * 4);
+  r.rew = (float*)take((size_t)C * 4);
+  r.done = (float*)take((size_t)C * 4);
+  r.cur_rows = (uint32_t*)take((size_t)B * N * 4);
+  r.cur_ctx = (double*)take((size_t)B * 4 * 8);
+  return r;
+}
+
+static size_t compact_bytes(int N, int C, int B) {
+  size_t o = 0;
+  auto take = [&](size_t bytes) { o = align_up(o + bytes, 256); };
+  take((size_t)C * N * 4); take((size_t)C * N * 4); take((size_t)C * 32); take((size_t)C * 32);
+  take((size_t)C * 4); take((size_t)C * 4); take((size_t)C * 4); take((size_t)C * 4);
+  take((size_t)B * N * 4); take((size_t)B * 32);
+  return o;
+}
+
+// pack episode e's current state (spins, local field, time-since-flip counts, scalars) into rows / ctx
+__device__ __forceinline__ void compact_pack(const eco_env_config& cfg, const EnvLayout& L, const uint8_t* state, int e,
+                                             uint32_t* rows, double* ctx, int32_t* err) {
+  const int N = L.N;
+  const int8_t* sp = (const int8_t*)(state + L.off_spins) + (size_t)e * N;
+  const int32_t* hf = (const int32_t*)(state + L.off_field) + (size_t)e * N;
+  const int16_t* ts = (const int16_t*)(state + L.off_tsf) + (size_t)e * N;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) {
+    const int h = hf[v];
+    if (h < -32768 || h > 32767) atomicCAS(err, 0, ECO_ERR_GRAPH);  // compact rows need |J s| < 2^15
+    rows[v] = (sp[v] < 0 ? 0x80000000u : 0u) | ((uint32_t)(ts[v] & 0x7FFF) << 16) | ((uint32_t)h & 0xFFFFu);
+  }
+  if (threadIdx.x == 0) {
+    const EpScal* sc = (const EpScal*)(state + L.off_scal) + e;
+    const int t = sc->t;
+    double dist = 0.0, term = 0.0;  // a reset state's rows are 0 (_reset_state never sets them)
+    if (t > 0) {
+      const double dsc = sc->score - sc->best_score;
+      dist = (dsc < 0.0 ? -dsc : dsc) / sc->mlr;                          // spinsystem.py:516-519
+      const double x = (double)(t - cfg.max_steps) / (double)cfg.horizon_length + 1.0;
+      term = x > 0.0 ? x : 0.0;                                           // :509-511
+    }
+    ctx[0] = dist; ctx[1] = term; ctx[2] = (double)t; ctx[3] = (double)sc->hamming;
+  }
+}
+
+__global__ __launch_bounds__(256) void replay_compact_snapshot_kernel(eco_env_config cfg, EnvLayout L, const uint8_t* state,
+                                                                      CompactRing r, const uint8_t* mask, int32_t* err) {
+  const int e = blockIdx.x;
+  if (mask && !mask[e]) return;
+  compact_pack(cfg, L, state, e, r.cur_rows + (size_t)e * L.N, r.cur_ctx + (size_t)e * 4, err);
+}
+
+__global__ __launch_bounds__(256) void replay_compact_push_kernel(eco_env_config cfg, EnvLayout L, const uint8_t* state,
+                                                                  CompactRing r, int C, int pos, const int32_t* actions,
+                                                                  const double* rewards, const uint8_t* dones,
+                                                                  int32_t* err) {
+  const int e = blockIdx.x;
+  const int N = L.N;
+  const int slot = (int)(((long long)pos + e) % C);
+  uint32_t* cur = r.cur_rows + (size_t)e * N;
+  uint32_t* rs = r.rows_s + (size_t)slot * N;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) rs[v] = cur[v];  // s = the state the action was taken in
+  if (threadIdx.x < 4) r.ctx_s[(size_t)slot * 4 + threadIdx.x] = r.cur_ctx[(size_t)e * 4 + threadIdx.x];
+  __syncthreads();
+  compact_pack(cfg, L, state, e, cur, r.cur_ctx + (size_t)e * 4, err);  // s' becomes the current state
+  __syncthreads();
+  uint32_t* rn = r.rows_n + (size_t)slot * N;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) rn[v] = cur[v];
+  if (threadIdx.x < 4) r.ctx_n[(size_t)slot * 4 + threadIdx.x] = r.cur_ctx[(size_t)e * 4 + threadIdx.x];
+  if (threadIdx.x == 0) {
+    r.gid[slot] = ((const EpScal*)(state + L.off_scal) + e)->graph;
+    r.act[slot] = actions[e];
+    r.rew[slot] = (float)rewards[e];  // torch.as_tensor([reward], dtype=torch.float) (dqn.py:299)
+    r.done[slot] = dones[e] ? 1.f : 0.f;
+  }
+}
+
+// feature rows of one compact state, written exactly as write_obs does (same obs_value, same casts)
+__device__ __forceinline__ void compact_expand(const eco_env_config& cfg, const uint32_t* rows, const double* ctx,
+                                               double mlr, const double* tab, int N, float* out, int* red) {
+  int cnt = 0;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) {
+    const uint32_t w = rows[v];
+    const int sv = (w >> 31) ? -1 : 1;
+    const int h = (int)(int16_t)(w & 0xFFFFu);
+    cnt += (sv * h > 0);
+  }
+  cnt = wave_sum_i(cnt);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  int total = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) total += red[k];
+  __syncthreads();
+  ObsCtx c;
+  c.mlr = mlr; c.dist_best = ctx[0]; c.term = ctx[1]; c.hamming = ctx[3];
+  const int t = (int)ctx[2];
+  c.ep_time = tab[t];
+  c.nqi = (double)total / (double)N;
+  c.basis = cfg.spin_basis;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) {
+    const uint32_t w = rows[v];
+    const int sv = (w >> 31) ? -1 : 1;
+    const int tsfk = (int)((w >> 16) & 0x7FFFu);
+    const int h = (int)(int16_t)(w & 0xFFFFu);
+    float xf[ECO_MAX_OBS];
+#pragma unroll
+    for (int i = 0; i < ECO_MAX_OBS; ++i) xf[i] = i < cfg.n_obs ? (float)obs_value(cfg.obs_ids[i], c, sv, h, tsfk, tab) : 0.f;
+    store_obs_row(out, (size_t)v, cfg.n_obs, xf);
+  }
+}
+
+// grid (2, M): blockIdx.x = 0 rebuilds s, 1 rebuilds s' of the m-th sampled transition (the same distinct
+// Feistel slots as replay_sample_kernel)
+__global__ __launch_bounds__(256) void replay_compact_sample_kernel(eco_env_config cfg, CompactRing r, int size, int M,
+                                                                    uint64_t key, const double* tab, eco_graph_set gs,
+                                                                    float* xs, float* xn, int32_t* gid, int32_t* act,
+                                                                    float* rew, float* done) {
+  __shared__ int red[4];
+  const int m = blockIdx.y;
+  if (m >= M) return;
+  int bits = 2;
+  while ((1 << bits) < size) ++bits;
+  if (bits & 1) ++bits;
+  const int half = bits / 2;
+  uint32_t x = (uint32_t)m;
+  do { x = feistel(x, half, key); } while (x >= (uint32_t)size);
+  const int slot = (int)x;
+  const int N = cfg.n_spins;
+  const int W = ECO_OBS_X_STRIDE(cfg.n_obs);
+  const int g = r.gid[slot];
+  const double mlr = gs.meta[(size_t)g * 4];
+  if (blockIdx.x == 0) {
+    compact_expand(cfg, r.rows_s + (size_t)slot * N, r.ctx_s + (size_t)slot * 4, mlr, tab, N, xs + (size_t)m * N * W, red);
+    if (threadIdx.x == 0) { gid[m] = g; act[m] = r.act[slot]; rew[m] = r.rew[slot]; done[m] = r.done[slot]; }
+  } else {
+    compact_expand(cfg, r.rows_n + (size_t)slot * N, r.ctx_n + (size_t)slot * 4, mlr, tab, N, xn + (size_t)m * N * W, red);
+  }
+}
+
 static size_t slab_bytes() { return (size_t)MAX_JOBS * SLABS_PER_JOB * SLAB * sizeof(float); }
 
 }  // namespace eco
@@ -553,6 +717,7 @@ extern "C" int eco_replay_push(const eco_replay* rb, int32_t pos, int32_t batch,
   if (!rb || !xs || !xn || !graph_ids || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
   if (rb->x_stride != 0 && rb->x_stride != 8 && rb->x_stride != 16) return fail(ECO_ERR_ARG, "x_stride must be 8 or 16");
   if (batch < 1 || rb->capacity < 1 || pos < 0) return fail(ECO_ERR_ARG, "bad batch/capacity/pos");
+  if (batch > rb->capacity) return fail(ECO_ERR_ARG, "replay push: batch larger than the ring (slots would collide)");
   replay_push_kernel<<<dim3(1, batch), 256, 0, (hipStream_t)stream>>>(*rb, pos, batch, xs, xn, graph_ids, actions,
                                                                       rewards, dones);
   return check_launch("replay_push");
@@ -568,4 +733,60 @@ extern "C" int eco_replay_sample(const eco_replay* rb, int32_t size, int32_t m, 
   replay_sample_kernel<<<dim3(1, m), 256, 0, (hipStream_t)stream>>>(*rb, size, m, rng3(seed, counter, 0x5A5A),
                                                                     xs, xn, graph_ids, actions, rewards, dones);
   return check_launch("replay_sample");
+}
+
+static int compact_check(const eco_env_config* cfg, int32_t batch, int32_t capacity) {
+  if (!cfg) return fail(ECO_ERR_ARG, "null config");
+  if (cfg->optimisation_target != ECO_TARGET_CUT) return fail(ECO_ERR_TARGET, "compact replay: OptimisationTarget.CUT only");
+  if (cfg->max_steps > 32767) return fail(ECO_ERR_ARG, "compact replay: max_steps must be < 32768");
+  if (batch < 1 || capacity < 1) return fail(ECO_ERR_ARG, "bad batch/capacity");
+  return ECO_OK;
+}
+
+extern "C" size_t eco_replay_compact_bytes(int32_t n_spins, int32_t capacity, int32_t batch) {
+  if (n_spins < 1 || capacity < 1 || batch < 1) return 0;
+  return compact_bytes(n_spins, capacity, batch);
+}
+
+extern "C" int eco_replay_compact_snapshot(const eco_env_config* cfg, const void* env_state, int32_t batch, void* ring,
+                                           int32_t capacity, const uint8_t* mask, eco_stream_t stream) {
+  int rc = compact_check(cfg, batch, capacity);
+  if (rc) return rc;
+  if (!env_state || !ring) return fail(ECO_ERR_ARG, "null state/ring");
+  const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, batch);
+  replay_compact_snapshot_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(
+      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, capacity, batch), mask, err_word());
+  return check_launch("replay_compact_snapshot");
+}
+
+extern "C" int eco_replay_compact_push(const eco_env_config* cfg, const void* env_state, int32_t batch, void* ring,
+                                       int32_t capacity, int32_t pos, const int32_t* actions, const double* rewards,
+                                       const uint8_t* dones, eco_stream_t stream) {
+  int rc = compact_check(cfg, batch, capacity);
+  if (rc) return rc;
+  if (!env_state || !ring || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
+  if (pos < 0 || batch > capacity) return fail(ECO_ERR_ARG, "replay push: bad position or batch larger than the ring");
+  const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, batch);
+  replay_compact_push_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(
+      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, capacity, batch), capacity, pos, actions,
+      rewards, dones, err_word());
+  return check_launch("replay_compact_push");
+}
+
+extern "C" int eco_replay_compact_sample(const eco_env_config* cfg, const void* env_state, const eco_graph_set* gs,
+                                         int32_t env_batch, const void* ring, int32_t capacity, int32_t size, int32_t m,
+                                         uint64_t seed, uint64_t counter, float* xs, float* xn, int32_t* graph_ids,
+                                         int32_t* actions, float* rewards, float* dones, eco_stream_t stream) {
+  int rc = compact_check(cfg, env_batch, capacity);
+  if (rc) return rc;
+  if (!env_state || !gs || !ring || !xs || !xn || !graph_ids || !actions || !rewards || !dones)
+    return fail(ECO_ERR_ARG, "null argument");
+  if (size < m || m < 1 || size > capacity)
+    return fail(ECO_ERR_ARG, "replay sample: need m <= size <= capacity (random.sample without replacement)");
+  const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, env_batch);
+  const double* tab = (const double*)((const uint8_t*)env_state + L.off_tab + 256);
+  replay_compact_sample_kernel<<<dim3(2, m), 256, 0, (hipStream_t)stream>>>(
+      *cfg, compact_carve(const_cast<void*>(ring), cfg->n_spins, capacity, env_batch), size, m,
+      rng3(seed, counter, 0x5A5A), tab, *gs, xs, xn, graph_ids, actions, rewards, dones);
+  return check_launch("replay_compact_sample");
 }

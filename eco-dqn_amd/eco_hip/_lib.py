@@ -95,6 +95,12 @@ _SIG = {
     "eco_replay_push": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "eco_replay_sample": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P,
                                          _P, _P, _P, _P, _P]),
+    "eco_replay_compact_bytes": (ctypes.c_size_t, [_I, _I, _I]),
+    "eco_replay_compact_snapshot": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, _P, _P]),
+    "eco_replay_compact_push": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "eco_replay_compact_sample": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, ctypes.POINTER(GraphSet), _I, _P, _I,
+                                                 _I, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _P, _P,
+                                                 _P]),
     "eco_last_error": (ctypes.c_char_p, []),
 }
 for _name, (_res, _args) in _SIG.items():

@@ -26,7 +26,7 @@ import torch
 
 from ... import _lib
 from ...parallel import allreduce_gradients, broadcast_parameters
-from .utils import ReplayBuffer, TestMetric, set_global_seed
+from .utils import CompactReplayBuffer, ReplayBuffer, TestMetric, set_global_seed
 
 
 class DQN:
@@ -39,7 +39,8 @@ class DQN:
                  final_exploration_step=1000000, adam_epsilon=1e-8, loss="mse", save_network_frequency=10000,
                  network_save_path='network', evaluate=True, test_envs=None, test_episodes=20,
                  test_frequency=10000, test_save_path='test_scores', test_metric=TestMetric.ENERGY_ERROR,
-                 logging=True, seed=None, train_minibatch=None, graph_pool_ids=None, regenerate_graphs=None):
+                 logging=True, seed=None, train_minibatch=None, graph_pool_ids=None, regenerate_graphs=None,
+                 compact_replay=None):
         if isinstance(envs, (list, tuple)):
             if len(envs) != 1:
                 raise NotImplementedError("pass one VecSpinSystem (it already holds B episodes)")
@@ -99,8 +100,17 @@ class DQN:
         self.B = envs.n_envs
         self.N = envs.n_spins
         self.M = int(train_minibatch or minibatch_size)
-        self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed,
-                                          n_obs=envs.n_obs)
+        # compact replay (integer env state, 8 B per vertex) for MaxCut envs on +-1 graphs; else fp32 features
+        eligible = (envs.cfg.optimisation_target == _lib.ECO_TARGET_CUT and envs.graphs.unit_weights
+                    and envs.max_steps < 32768)
+        self.compact_replay = eligible if compact_replay is None else bool(compact_replay)
+        if self.compact_replay and not eligible:
+            raise ValueError("compact replay needs OptimisationTarget.CUT, +-1 weights and max_steps < 32768")
+        if self.compact_replay:
+            self.replay_buffer = CompactReplayBuffer(replay_buffer_size, envs, seed=self.seed)
+        else:
+            self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed,
+                                              n_obs=envs.n_obs)
         self.replay_ratio = minibatch_size / float(update_frequency)
         # reference: one target sync per update_target_frequency env-steps = that many
         # env-steps' worth of replayed samples
@@ -263,15 +273,24 @@ class DQN:
         nxt = self._obs[1] if x.data_ptr() == self._obs[0].data_ptr() else self._obs[0]
         self.act(x, self.env.graph_ids, is_training_ready, actions_out=self._actions)
         _, rew, done = self.env.step(self._actions, obs_out=nxt)
-        self.replay_buffer.add_batch(x, nxt, self.env.graph_ids, self._actions, rew, done)
+        if self.compact_replay:
+            self.replay_buffer.add_step(self._actions, rew, done)
+        else:
+            self.replay_buffer.add_batch(x, nxt, self.env.graph_ids, self._actions, rew, done)
         self._pushed += self.B
         return nxt
+
+    def _reset_env(self, graph_ids, seed, mask=None):
+        """env.reset (all episodes, or the masked ones) and, for the compact replay, record the new states."""
+        self.env.reset(graph_ids=graph_ids, mask=mask, seed=seed)
+        if self.compact_replay:
+            self.replay_buffer.snapshot(mask)
 
     def start(self):
         """Reset every episode on fresh pool graphs (start of learn)."""
         self._pushed = 0
         self._half_last_push = [-(1 << 62), -(1 << 62)]
-        self.env.reset(graph_ids=self._switch_graph_half(self.B), seed=self.seed)
+        self._reset_env(self._switch_graph_half(self.B), self.seed)
         self._steps_in_episode = 0
         self._timestep = 0
         self._ready = False
@@ -298,16 +317,16 @@ class DQN:
             self.update_lr(self._timestep)
         if self._lockstep:
             if self._steps_in_episode == T:
-                self.env.reset(graph_ids=self._switch_graph_half(B), seed=self.seed + self._timestep)
+                self._reset_env(self._switch_graph_half(B), self.seed + self._timestep)
                 self._steps_in_episode = 0
         else:
             done = self.env.dones.bool()
             n_done = int(done.sum())
             if n_done == B:
-                self.env.reset(graph_ids=self._switch_graph_half(B), seed=self.seed + self._timestep)
+                self._reset_env(self._switch_graph_half(B), self.seed + self._timestep)
                 self._steps_in_episode = 0
             elif n_done:
-                self.env.reset(graph_ids=self._random_graph_ids(B), mask=done, seed=self.seed + self._timestep)
+                self._reset_env(self._random_graph_ids(B), self.seed + self._timestep, mask=done)
         if self._ready:
             step_losses = []
             for _ in range(self._k_per_vec):

@@ -229,7 +229,7 @@ def test_learn_s2v_resets_finished_episodes():
     n, B = 20, 64
     store = GraphStore.random("ER", 256, n, 0.15, seed=9)
     env = _s2v_env(store, n, B, T=2 * n)
-    agent = _s2v_dqn(env, replay_buffer_size=B * 2 * n * 4, replay_start_size=B * n)
+    agent = _s2v_dqn(env, replay_buffer_size=B * 2 * n * 4, replay_start_size=B * n, compact_replay=False)
     agent.start()
     for _ in range(3 * n):
         agent.iteration()
@@ -351,3 +351,49 @@ def test_learn_evaluates_saves_and_pickles(tmp_path):
     # the saved checkpoint is a plain state_dict with the reference's keys
     sd = torch.load(tmp_path / f"network{B * 40}.pth", map_location="cpu", weights_only=True)
     assert list(sd) == mo.KEYS
+
+
+@pytest.mark.parametrize("n,B,basis", [(20, 64, "SIGNED"), (200, 16, "BINARY")])
+def test_compact_replay_matches_feature_replay(n, B, basis):
+    """The compact replay (integer env state per transition, features rebuilt on sample) returns exactly
+    the transitions the fp32 feature ring returns for the same pushes and the same sampling keys: node
+    features bitwise, actions, rewards, dones, graph ids -- across a masked reset (new s rows) and a
+    ring wrap.  The compact ring stores 8 B per vertex per transition against 64 B."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.agents.dqn.utils import ReplayBuffer, CompactReplayBuffer
+    store = GraphStore.random("ER", 2 * B, n, 0.15, seed=n)
+    env = VecSpinSystem(store, B, 2 * n, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis[basis], norm_rewards=True, basin_reward=1. / n)
+    C = B * 5
+    feat = ReplayBuffer(C, n, device="cuda", seed=17)
+    comp = CompactReplayBuffer(C, env, seed=17)
+    # bytes: 8 per vertex per transition (+ scalars, + the current state of each episode) vs 64
+    assert comp.ring.numel() * 4 < C * n * 2 * 8 * 4
+    env.reset(graph_ids=np.arange(B), seed=3)
+    comp.snapshot()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = env.obs_x.clone()
+    for t in range(8):
+        acts = torch.randint(0, n, (B,), generator=g, device="cuda", dtype=torch.int32)
+        nxt = torch.empty_like(x)
+        _, rew, done = env.step(acts, obs_out=nxt)
+        feat.add_batch(x, nxt, env.graph_ids, acts, rew, done)
+        comp.add_step(acts, rew, done)
+        x = nxt.clone()
+        if t == 3:  # masked reset of half the episodes onto new graphs
+            mask = (torch.arange(B, device="cuda") % 2).to(torch.uint8)
+            env.reset(graph_ids=np.arange(B) + B, mask=mask, seed=9)
+            comp.snapshot(mask)
+            x = env.obs_x.clone()
+    env.check_errors()
+    assert len(feat) == len(comp) == C
+    for m in (C // 2, C):
+        a = feat.sample(m)
+        b = comp.sample(m)
+        for u, v in zip(a, b):
+            assert torch.equal(u.view(torch.int32) if u.dtype == torch.float32 else u,
+                               v.view(torch.int32) if v.dtype == torch.float32 else v)
