@@ -133,7 +133,7 @@ def cpu_refcost_baseline(n=200, seconds=10.0):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "train_v4", "pmc_hbm.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "train", "pmc_hbm.json")
 PMC_SQ = os.path.join(REPO, "profiles", "r02", "train", "pmc_sq_dense.json")
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (~2.5 PF)
 
@@ -425,7 +425,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r01/train_v4/pmc_hbm.json)",
+                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r02/train/pmc_hbm.json)",
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},

@@ -454,50 +454,55 @@ __global__ void replay_sample_kernel(eco_replay rb, int size, int M, uint64_t ke
 
 // ------------------------------------------------------------ compact replay ----
 // ReplayBuffer of MaxCut (OptimisationTarget.CUT) transitions as the env's integer state instead of fp32
-// feature rows: per vertex one u32 {spin sign bit 31 | time-since-flip count bits 16..30 | local field
-// h = (J s)_v as int16 bits 0..15} for s and for s', plus per state {|score - best| / mlr, termination
-// immanency, step t, Hamming distance to the best spins} -- 8 B per vertex per transition against 64 B of
-// the feature ring.  The sample kernel rebuilds the fp32 feature rows with the env's own obs_value (the
-// same float64 operations, so the features equal, bit for bit, the rows the env wrote).
-// Ring: rows_s [C][N] u32 | rows_n [C][N] u32 | ctx_s [C][4] f64 | ctx_n [C][4] f64 | gid | act | rew | done
-// [C] | the current state of each env episode: cur_rows [B][N] u32 | cur_ctx [B][4] f64.
+// feature rows.  A transition stores ONE state: s, per vertex one u32 {spin sign bit 31 | time-since-flip
+// count bits 16..30 | local field h = (J s)_v as int16 bits 0..15}; s' is a deterministic function of s, the
+// action and the graph (env_step_kernel: flip spin a, reset its count, count +1 elsewhere, h_j -= 2 w_aj s_a
+// over the CSR row of a), rebuilt on sample.  Per state the scalars {|score - best| / mlr, termination
+// immanency, step t, Hamming distance to the best spins} are stored for s and s' (the Hamming distance needs
+// the best spins, which are not kept).  4N + 80 B per transition (880 B at N=200) against 64N of the feature
+// ring.  The sample kernel rebuilds the fp32 feature rows with the env's own obs_value (the same float64
+// operations, so the features equal, bit for bit, the rows the env wrote).
+// Ring of P = capacity + batch slots; transition k (k-th push, counted over the buffer's life) lives in slot
+// k % P.  push(k0) writes the s' of episode e straight into slot (k0 + batch + e) % P as the s of that
+// episode's next transition (a reset overwrites it through snapshot), so s is never copied; the `batch`
+// slots ahead of the newest transition are never sampled (size <= capacity = P - batch).
+// Layout: rows [P][N] u32 | ctx_s [P][4] f64 | ctx_n [P][4] f64 | gid | act | rew | done [P].
+// act bit 30 marks a transition whose step left the state unchanged (an auto-masked finished episode).
+constexpr uint32_t CR_NOFLIP = 0x40000000u;
+
 struct CompactRing {
-  uint32_t *rows_s, *rows_n, *cur_rows;
-  double *ctx_s, *ctx_n, *cur_ctx;
+  uint32_t* rows;
+  double *ctx_s, *ctx_n;
   int32_t *gid, *act;
   float *rew, *done;
 };
 
-static CompactRing compact_carve(void* base, int N, int C, int B) {
+static CompactRing compact_carve(void* base, int N, long long P, size_t* bytes = nullptr) {
   CompactRing r;
-  size_t o = 0;
   char* b = (char*)base;
-  auto take = [&](size_t bytes) { void* p = b + o; o = align_up(o + bytes, 256); return p; };
-  r.rows_s = (uint32_t*)take((size_t)C * N * 4);
-  r.rows_n = (uint32_t*)take((size_t)C * N * 4);
-  r.ctx_s = (double*)take((size_t)C * 4 * 8);
-  r.ctx_n = (double*)take((size_t)C * 4 * 8);
-  r.gid = (int32_t*)take((size_t)C * 4);
-  r.act = (int32_t*)take((size_t)C * 4);
-  r.rew = (float*)take((size_t)C * 4);
-  r.done = (float*)take((size_t)C * 4);
-  r.cur_rows = (uint32_t*)take((size_t)B * N * 4);
-  r.cur_ctx = (double*)take((size_t)B * 4 * 8);
+  size_t o = 0;
+  auto t = [&](size_t n) { void* p = b + o; o = align_up(o + n, 256); return p; };
+  r.rows = (uint32_t*)t((size_t)P * N * 4);
+  r.ctx_s = (double*)t((size_t)P * 32);
+  r.ctx_n = (double*)t((size_t)P * 32);
+  r.gid = (int32_t*)t((size_t)P * 4);
+  r.act = (int32_t*)t((size_t)P * 4);
+  r.rew = (float*)t((size_t)P * 4);
+  r.done = (float*)t((size_t)P * 4);
+  if (bytes) *bytes = o;
   return r;
 }
 
-static size_t compact_bytes(int N, int C, int B) {
+static size_t compact_bytes(int N, long long P) {
   size_t o = 0;
-  auto take = [&](size_t bytes) { o = align_up(o + bytes, 256); };
-  take((size_t)C * N * 4); take((size_t)C * N * 4); take((size_t)C * 32); take((size_t)C * 32);
-  take((size_t)C * 4); take((size_t)C * 4); take((size_t)C * 4); take((size_t)C * 4);
-  take((size_t)B * N * 4); take((size_t)B * 32);
+  compact_carve(nullptr, N, P, &o);
   return o;
 }
 
-// pack episode e's current state (spins, local field, time-since-flip counts, scalars) into rows / ctx
+// pack episode e's current state (spins, local field, time-since-flip counts, scalars) into rows / ctx (and
+// ctx2 when given: the same scalars as the s' of the transition just taken)
 __device__ __forceinline__ void compact_pack(const eco_env_config& cfg, const EnvLayout& L, const uint8_t* state, int e,
-                                             uint32_t* rows, double* ctx, int32_t* err) {
+                                             uint32_t* rows, double* ctx, double* ctx2, int32_t* err) {
   const int N = L.N;
   const int8_t* sp = (const int8_t*)(state + L.off_spins) + (size_t)e * N;
   const int32_t* hf = (const int32_t*)(state + L.off_field) + (size_t)e * N;
@@ -507,7 +512,7 @@ __device__ __forceinline__ void compact_pack(const eco_env_config& cfg, const En
     if (h < -32768 || h > 32767) atomicCAS(err, 0, ECO_ERR_GRAPH);  // compact rows need |J s| < 2^15
     rows[v] = (sp[v] < 0 ? 0x80000000u : 0u) | ((uint32_t)(ts[v] & 0x7FFF) << 16) | ((uint32_t)h & 0xFFFFu);
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 4) {
     const EpScal* sc = (const EpScal*)(state + L.off_scal) + e;
     const int t = sc->t;
     double dist = 0.0, term = 0.0;  // a reset state's rows are 0 (_reset_state never sets them)
@@ -517,40 +522,42 @@ __device__ __forceinline__ void compact_pack(const eco_env_config& cfg, const En
       const double x = (double)(t - cfg.max_steps) / (double)cfg.horizon_length + 1.0;
       term = x > 0.0 ? x : 0.0;                                           // :509-511
     }
-    ctx[0] = dist; ctx[1] = term; ctx[2] = (double)t; ctx[3] = (double)sc->hamming;
+    const double v = threadIdx.x == 0 ? dist : threadIdx.x == 1 ? term : threadIdx.x == 2 ? (double)t
+                                                                                          : (double)sc->hamming;
+    ctx[threadIdx.x] = v;
+    if (ctx2) ctx2[threadIdx.x] = v;
   }
 }
 
+__device__ __forceinline__ long long cr_slot(long long k, long long P) { return k % P; }
+
 __global__ __launch_bounds__(256) void replay_compact_snapshot_kernel(eco_env_config cfg, EnvLayout L, const uint8_t* state,
-                                                                      CompactRing r, const uint8_t* mask, int32_t* err) {
+                                                                      CompactRing r, long long P, long long pushed,
+                                                                      const uint8_t* mask, int32_t* err) {
   const int e = blockIdx.x;
   if (mask && !mask[e]) return;
-  compact_pack(cfg, L, state, e, r.cur_rows + (size_t)e * L.N, r.cur_ctx + (size_t)e * 4, err);
+  const long long slot = cr_slot(pushed + e, P);
+  compact_pack(cfg, L, state, e, r.rows + slot * L.N, r.ctx_s + slot * 4, nullptr, err);
 }
 
 __global__ __launch_bounds__(256) void replay_compact_push_kernel(eco_env_config cfg, EnvLayout L, const uint8_t* state,
-                                                                  CompactRing r, int C, int pos, const int32_t* actions,
-                                                                  const double* rewards, const uint8_t* dones,
-                                                                  int32_t* err) {
+                                                                  CompactRing r, long long P, long long pushed, int B,
+                                                                  const int32_t* actions, const double* rewards,
+                                                                  const uint8_t* dones, int32_t* err) {
   const int e = blockIdx.x;
   const int N = L.N;
-  const int slot = (int)(((long long)pos + e) % C);
-  uint32_t* cur = r.cur_rows + (size_t)e * N;
-  uint32_t* rs = r.rows_s + (size_t)slot * N;
-  for (int v = threadIdx.x; v < N; v += blockDim.x) rs[v] = cur[v];  // s = the state the action was taken in
-  if (threadIdx.x < 4) r.ctx_s[(size_t)slot * 4 + threadIdx.x] = r.cur_ctx[(size_t)e * 4 + threadIdx.x];
-  __syncthreads();
-  compact_pack(cfg, L, state, e, cur, r.cur_ctx + (size_t)e * 4, err);  // s' becomes the current state
-  __syncthreads();
-  uint32_t* rn = r.rows_n + (size_t)slot * N;
-  for (int v = threadIdx.x; v < N; v += blockDim.x) rn[v] = cur[v];
-  if (threadIdx.x < 4) r.ctx_n[(size_t)slot * 4 + threadIdx.x] = r.cur_ctx[(size_t)e * 4 + threadIdx.x];
+  const long long slot = cr_slot(pushed + e, P), next = cr_slot(pushed + B + e, P);
   if (threadIdx.x == 0) {
+    const int a = actions[e];
+    // did the step flip spin a (s' != s)?  An auto-masked finished episode returns its state unchanged.
+    const bool flipped = a >= 0 && a < N &&
+                         ((r.rows[slot * N + a] >> 31) != (uint32_t)(((const int8_t*)(state + L.off_spins))[(size_t)e * N + a] < 0));
     r.gid[slot] = ((const EpScal*)(state + L.off_scal) + e)->graph;
-    r.act[slot] = actions[e];
+    r.act[slot] = (int32_t)((uint32_t)a | (flipped ? 0u : CR_NOFLIP));
     r.rew[slot] = (float)rewards[e];  // torch.as_tensor([reward], dtype=torch.float) (dqn.py:299)
     r.done[slot] = dones[e] ? 1.f : 0.f;
   }
+  compact_pack(cfg, L, state, e, r.rows + next * N, r.ctx_s + next * 4, r.ctx_n + slot * 4, err);
 }
 
 // feature rows of one compact state, written exactly as write_obs does (same obs_value, same casts)
@@ -568,7 +575,6 @@ __device__ __forceinline__ void compact_expand(const eco_env_config& cfg, const 
   __syncthreads();
   int total = 0;
   for (int k = 0; k < (int)(blockDim.x >> 6); ++k) total += red[k];
-  __syncthreads();
   ObsCtx c;
   c.mlr = mlr; c.dist_best = ctx[0]; c.term = ctx[1]; c.hamming = ctx[3];
   const int t = (int)ctx[2];
@@ -587,12 +593,16 @@ __device__ __forceinline__ void compact_expand(const eco_env_config& cfg, const 
   }
 }
 
-// grid (2, M): blockIdx.x = 0 rebuilds s, 1 rebuilds s' of the m-th sampled transition (the same distinct
-// Feistel slots as replay_sample_kernel)
-__global__ __launch_bounds__(256) void replay_compact_sample_kernel(eco_env_config cfg, CompactRing r, int size, int M,
+// grid (2, M): blockIdx.x = 0 rebuilds s, 1 rebuilds s' of the m-th sampled transition.  The Feistel index x
+// names the slot the fp32 feature ring would read (replay_sample_kernel: slot x of a ring of `capacity`
+// written at k % capacity); here it is resolved to the transition k == x (mod capacity) among the newest
+// `size` and read from slot k % P.
+__global__ __launch_bounds__(256) void replay_compact_sample_kernel(eco_env_config cfg, CompactRing r, long long P,
+                                                                    int capacity, int size, long long pushed, int M,
                                                                     uint64_t key, const double* tab, eco_graph_set gs,
                                                                     float* xs, float* xn, int32_t* gid, int32_t* act,
                                                                     float* rew, float* done) {
+  extern __shared__ uint32_t cr_lds[];
   __shared__ int red[4];
   const int m = blockIdx.y;
   if (m >= M) return;
@@ -602,17 +612,46 @@ __global__ __launch_bounds__(256) void replay_compact_sample_kernel(eco_env_conf
   const int half = bits / 2;
   uint32_t x = (uint32_t)m;
   do { x = feistel(x, half, key); } while (x >= (uint32_t)size);
-  const int slot = (int)x;
+  const long long base = pushed - size;  // oldest transition still held
+  const long long k = base + (((long long)x - base % capacity) % capacity + capacity) % capacity;
+  const long long slot = cr_slot(k, P);
   const int N = cfg.n_spins;
   const int W = ECO_OBS_X_STRIDE(cfg.n_obs);
   const int g = r.gid[slot];
   const double mlr = gs.meta[(size_t)g * 4];
+  const uint32_t* rows = r.rows + slot * N;
+  const uint32_t av = (uint32_t)r.act[slot];
+  const int a = (int)(av & ~CR_NOFLIP);
   if (blockIdx.x == 0) {
-    compact_expand(cfg, r.rows_s + (size_t)slot * N, r.ctx_s + (size_t)slot * 4, mlr, tab, N, xs + (size_t)m * N * W, red);
-    if (threadIdx.x == 0) { gid[m] = g; act[m] = r.act[slot]; rew[m] = r.rew[slot]; done[m] = r.done[slot]; }
-  } else {
-    compact_expand(cfg, r.rows_n + (size_t)slot * N, r.ctx_n + (size_t)slot * 4, mlr, tab, N, xn + (size_t)m * N * W, red);
+    compact_expand(cfg, rows, r.ctx_s + slot * 4, mlr, tab, N, xs + (size_t)m * N * W, red);
+    if (threadIdx.x == 0) { gid[m] = g; act[m] = a; rew[m] = r.rew[slot]; done[m] = r.done[slot]; }
+    return;
   }
+  // s' = env step of s by a (env_step_kernel, spinsystem.py:397, :492-497): flip a, counts, local field
+  const bool flip = !(av & CR_NOFLIP);
+  const int sa_old = (rows[a] >> 31) ? -1 : 1;
+  for (int v = threadIdx.x; v < N; v += blockDim.x) {
+    uint32_t w = rows[v];
+    if (flip) {
+      const uint32_t tsfk = v == a ? 0u : (((w >> 16) & 0x7FFFu) + 1u) & 0x7FFFu;
+      w = ((v == a ? ~w : w) & 0x80000000u) | (tsfk << 16) | (w & 0xFFFFu);
+    }
+    cr_lds[v] = w;
+  }
+  __syncthreads();
+  if (flip) {
+    const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
+    const uint32_t* ed = gs.edges + gs.edge_base[g];
+    for (int q = rp[a] + threadIdx.x; q < rp[a + 1]; q += blockDim.x) {
+      const uint32_t ex = ed[q];
+      const int j = edge_col(ex);
+      const uint32_t w = cr_lds[j];
+      const int h = (int)(int16_t)(w & 0xFFFFu) - 2 * edge_w(ex) * sa_old;
+      cr_lds[j] = (w & 0xFFFF0000u) | ((uint32_t)h & 0xFFFFu);
+    }
+    __syncthreads();
+  }
+  compact_expand(cfg, cr_lds, r.ctx_n + slot * 4, mlr, tab, N, xn + (size_t)m * N * W, red);
 }
 
 static size_t slab_bytes() { return (size_t)MAX_JOBS * SLABS_PER_JOB * SLAB * sizeof(float); }
@@ -739,54 +778,60 @@ static int compact_check(const eco_env_config* cfg, int32_t batch, int32_t capac
   if (!cfg) return fail(ECO_ERR_ARG, "null config");
   if (cfg->optimisation_target != ECO_TARGET_CUT) return fail(ECO_ERR_TARGET, "compact replay: OptimisationTarget.CUT only");
   if (cfg->max_steps > 32767) return fail(ECO_ERR_ARG, "compact replay: max_steps must be < 32768");
+  if (cfg->n_spins < 1 || cfg->n_spins > ECO_COMPACT_MAX_SPINS) return fail(ECO_ERR_ARG, "compact replay: n_spins out of range");
   if (batch < 1 || capacity < 1) return fail(ECO_ERR_ARG, "bad batch/capacity");
   return ECO_OK;
 }
 
 extern "C" size_t eco_replay_compact_bytes(int32_t n_spins, int32_t capacity, int32_t batch) {
-  if (n_spins < 1 || capacity < 1 || batch < 1) return 0;
-  return compact_bytes(n_spins, capacity, batch);
+  if (n_spins < 1 || n_spins > ECO_COMPACT_MAX_SPINS || capacity < 1 || batch < 1) return 0;
+  return compact_bytes(n_spins, (long long)capacity + batch);
 }
 
 extern "C" int eco_replay_compact_snapshot(const eco_env_config* cfg, const void* env_state, int32_t batch, void* ring,
-                                           int32_t capacity, const uint8_t* mask, eco_stream_t stream) {
+                                           int32_t capacity, int64_t pushed, const uint8_t* mask, eco_stream_t stream) {
   int rc = compact_check(cfg, batch, capacity);
   if (rc) return rc;
-  if (!env_state || !ring) return fail(ECO_ERR_ARG, "null state/ring");
+  if (!env_state || !ring || pushed < 0) return fail(ECO_ERR_ARG, "null state/ring or negative push count");
   const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, batch);
+  const long long P = (long long)capacity + batch;
   replay_compact_snapshot_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(
-      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, capacity, batch), mask, err_word());
+      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, P), P, pushed, mask, err_word());
   return check_launch("replay_compact_snapshot");
 }
 
 extern "C" int eco_replay_compact_push(const eco_env_config* cfg, const void* env_state, int32_t batch, void* ring,
-                                       int32_t capacity, int32_t pos, const int32_t* actions, const double* rewards,
+                                       int32_t capacity, int64_t pushed, const int32_t* actions, const double* rewards,
                                        const uint8_t* dones, eco_stream_t stream) {
   int rc = compact_check(cfg, batch, capacity);
   if (rc) return rc;
   if (!env_state || !ring || !actions || !rewards || !dones) return fail(ECO_ERR_ARG, "null argument");
-  if (pos < 0 || batch > capacity) return fail(ECO_ERR_ARG, "replay push: bad position or batch larger than the ring");
+  if (pushed < 0 || batch > capacity) return fail(ECO_ERR_ARG, "replay push: negative push count or batch larger than the ring");
   const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, batch);
+  const long long P = (long long)capacity + batch;
   replay_compact_push_kernel<<<batch, 256, 0, (hipStream_t)stream>>>(
-      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, capacity, batch), capacity, pos, actions,
-      rewards, dones, err_word());
+      *cfg, L, (const uint8_t*)env_state, compact_carve(ring, cfg->n_spins, P), P, pushed, batch, actions, rewards,
+      dones, err_word());
   return check_launch("replay_compact_push");
 }
 
 extern "C" int eco_replay_compact_sample(const eco_env_config* cfg, const void* env_state, const eco_graph_set* gs,
-                                         int32_t env_batch, const void* ring, int32_t capacity, int32_t size, int32_t m,
-                                         uint64_t seed, uint64_t counter, float* xs, float* xn, int32_t* graph_ids,
-                                         int32_t* actions, float* rewards, float* dones, eco_stream_t stream) {
+                                         int32_t env_batch, const void* ring, int32_t capacity, int32_t size,
+                                         int64_t pushed, int32_t m, uint64_t seed, uint64_t counter, float* xs,
+                                         float* xn, int32_t* graph_ids, int32_t* actions, float* rewards, float* dones,
+                                         eco_stream_t stream) {
   int rc = compact_check(cfg, env_batch, capacity);
   if (rc) return rc;
   if (!env_state || !gs || !ring || !xs || !xn || !graph_ids || !actions || !rewards || !dones)
     return fail(ECO_ERR_ARG, "null argument");
-  if (size < m || m < 1 || size > capacity)
-    return fail(ECO_ERR_ARG, "replay sample: need m <= size <= capacity (random.sample without replacement)");
+  if (size < m || m < 1 || size > capacity || pushed < size)
+    return fail(ECO_ERR_ARG, "replay sample: need m <= size <= min(capacity, pushed) (random.sample without replacement)");
+  if (gs->n_spins != cfg->n_spins) return fail(ECO_ERR_ARG, "replay sample: graph set / env size mismatch");
   const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, env_batch);
   const double* tab = (const double*)((const uint8_t*)env_state + L.off_tab + 256);
-  replay_compact_sample_kernel<<<dim3(2, m), 256, 0, (hipStream_t)stream>>>(
-      *cfg, compact_carve(const_cast<void*>(ring), cfg->n_spins, capacity, env_batch), size, m,
+  const long long P = (long long)capacity + env_batch;
+  replay_compact_sample_kernel<<<dim3(2, m), 256, (size_t)cfg->n_spins * 4, (hipStream_t)stream>>>(
+      *cfg, compact_carve(const_cast<void*>(ring), cfg->n_spins, P), P, capacity, size, pushed, m,
       rng3(seed, counter, 0x5A5A), tab, *gs, xs, xn, graph_ids, actions, rewards, dones);
   return check_launch("replay_compact_sample");
 }

@@ -29,6 +29,7 @@ def obs_x_stride(n_obs):
     """ECO_OBS_X_STRIDE: floats per node-feature row of obs_x."""
     return 8 if n_obs <= 8 else 16
 ECO_MAX_SPINS = 2048
+ECO_COMPACT_MAX_SPINS = 8192  # include/eco_hip.h: compact replay (sample rebuilds s' in LDS)
 ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL = 0, 1
 ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
 
@@ -96,10 +97,12 @@ _SIG = {
     "eco_replay_sample": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P,
                                          _P, _P, _P, _P, _P]),
     "eco_replay_compact_bytes": (ctypes.c_size_t, [_I, _I, _I]),
-    "eco_replay_compact_snapshot": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, _P, _P]),
-    "eco_replay_compact_push": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "eco_replay_compact_snapshot": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, ctypes.c_int64, _P,
+                                                   _P]),
+    "eco_replay_compact_push": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _I, ctypes.c_int64, _P, _P, _P,
+                                               _P]),
     "eco_replay_compact_sample": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, ctypes.POINTER(GraphSet), _I, _P, _I,
-                                                 _I, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _P, _P,
+                                                 _I, ctypes.c_int64, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _P, _P,
                                                  _P]),
     "eco_last_error": (ctypes.c_char_p, []),
 }

@@ -100,12 +100,14 @@ class DQN:
         self.B = envs.n_envs
         self.N = envs.n_spins
         self.M = int(train_minibatch or minibatch_size)
-        # compact replay (integer env state, 8 B per vertex) for MaxCut envs on +-1 graphs; else fp32 features
+        # compact replay (one integer env state per transition, 4 B per vertex) for MaxCut envs on +-1
+        # graphs; else fp32 features
         eligible = (envs.cfg.optimisation_target == _lib.ECO_TARGET_CUT and envs.graphs.unit_weights
-                    and envs.max_steps < 32768)
+                    and envs.max_steps < 32768 and self.N <= _lib.ECO_COMPACT_MAX_SPINS)
         self.compact_replay = eligible if compact_replay is None else bool(compact_replay)
         if self.compact_replay and not eligible:
-            raise ValueError("compact replay needs OptimisationTarget.CUT, +-1 weights and max_steps < 32768")
+            raise ValueError("compact replay needs OptimisationTarget.CUT, +-1 weights, max_steps < 32768 and "
+                             f"n_spins <= {_lib.ECO_COMPACT_MAX_SPINS}")
         if self.compact_replay:
             self.replay_buffer = CompactReplayBuffer(replay_buffer_size, envs, seed=self.seed)
         else:

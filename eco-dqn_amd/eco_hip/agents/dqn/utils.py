@@ -95,10 +95,12 @@ class ReplayBuffer:
 
 class CompactReplayBuffer:
     """ReplayBuffer (dqn/utils.py:28-83) for MaxCut envs that stores each transition as the env's integer
-    state (include/eco_hip.h eco_replay_compact_*): per vertex spin, time-since-flip count and local field
-    for s and s' (8 B per vertex) plus four float64 per state, instead of fp32 feature rows (64 B per
-    vertex).  sample() rebuilds the feature rows bit-exactly on the device and returns the same tuple as
-    ReplayBuffer.sample.  Driven by the env: snapshot() after every reset, add_step() after every step."""
+    state (include/eco_hip.h eco_replay_compact_*): ONE state per transition -- per vertex spin,
+    time-since-flip count and local field in 4 B -- plus four float64 observation scalars for s and s'
+    (4N + 80 B per transition, 880 B at N=200, against 64N B of fp32 feature rows for s and s').  s' is
+    rebuilt from s, the action and the graph on sample, and both feature rows bit-exactly; sample() returns
+    the same tuple as ReplayBuffer.sample.  Driven by the env: snapshot() after every reset, add_step()
+    after every step."""
 
     def __init__(self, capacity, env, seed=0):
         self.env = env
@@ -106,11 +108,13 @@ class CompactReplayBuffer:
         self.n_spins = env.n_spins
         self.x_stride = _lib.obs_x_stride(env.n_obs)
         self.device = env.graphs.device
+        if env.n_envs > self._capacity:
+            raise ValueError("compact replay: capacity must hold at least one batch of transitions")
         nbytes = _lib.lib.eco_replay_compact_bytes(self.n_spins, self._capacity, env.n_envs)
         if nbytes == 0:
             raise ValueError("bad compact replay size")
         self.ring = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-        self._position = 0
+        self._pushed = 0  # transitions added over the buffer's life (the k-th lives in slot k % (capacity + B))
         self._size = 0
         self.seed = seed
         self._counter = 0
@@ -121,16 +125,16 @@ class CompactReplayBuffer:
         mk = None if mask is None else torch.as_tensor(mask, dtype=torch.uint8, device=self.device).contiguous()
         _lib.check(_lib.lib.eco_replay_compact_snapshot(ctypes.byref(self.env.cfg), _lib.ptr(self.env.state),
                                                         self.env.n_envs, _lib.ptr(self.ring), self._capacity,
-                                                        _lib.ptr(mk), _lib.stream_ptr(stream)))
+                                                        self._pushed, _lib.ptr(mk), _lib.stream_ptr(stream)))
 
     def add_step(self, actions, rewards, dones, stream=None):
         """ReplayBuffer.add (dqn/utils.py:39-47) of the transitions of the env step just taken."""
         B = self.env.n_envs
         _lib.check(_lib.lib.eco_replay_compact_push(ctypes.byref(self.env.cfg), _lib.ptr(self.env.state), B,
-                                                    _lib.ptr(self.ring), self._capacity, self._position,
+                                                    _lib.ptr(self.ring), self._capacity, self._pushed,
                                                     _lib.ptr(actions), _lib.ptr(rewards), _lib.ptr(dones),
                                                     _lib.stream_ptr(stream)))
-        self._position = (self._position + B) % self._capacity
+        self._pushed += B
         self._size = min(self._capacity, self._size + B)
 
     def _buffers(self, m):
@@ -149,10 +153,14 @@ class CompactReplayBuffer:
         self._counter += 1
         _lib.check(_lib.lib.eco_replay_compact_sample(
             ctypes.byref(self.env.cfg), _lib.ptr(self.env.state), ctypes.byref(self.env.graphs.gs), self.env.n_envs,
-            _lib.ptr(self.ring), self._capacity, self._size, batch_size, ctypes.c_uint64(self.seed),
+            _lib.ptr(self.ring), self._capacity, self._size, self._pushed, batch_size, ctypes.c_uint64(self.seed),
             ctypes.c_uint64(self._counter), _lib.ptr(xs), _lib.ptr(xn), _lib.ptr(gid), _lib.ptr(act), _lib.ptr(rew),
             _lib.ptr(done), _lib.stream_ptr(stream)))
         return xs, act, rew, xn, done, gid
+
+    @property
+    def bytes_per_transition(self):
+        return self.ring.numel() / (self._capacity + self.env.n_envs)
 
     def __len__(self):
         return self._size

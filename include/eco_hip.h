@@ -268,30 +268,35 @@ int eco_replay_sample(const eco_replay *rb, int32_t size, int32_t m, uint64_t se
                       float *xn, int32_t *graph_ids, int32_t *actions, float *rewards, float *dones,
                       eco_stream_t stream);
 
-/* Compact ReplayBuffer for MaxCut (OptimisationTarget.CUT) envs: transitions stored as the env's integer
- * state -- per vertex one u32 {spin sign | time-since-flip count | local field (J s)_v as int16} for s and s'
- * plus four f64 per state -- instead of fp32 feature rows (8 B vs 64 B per vertex per transition); the
- * sample rebuilds the feature rows bit-exactly with the env's own observation arithmetic
- * (spinsystem.py:486-535).  Same ReplayBuffer semantics (dqn/utils.py:28-83): ring of `capacity` slots,
- * add at (pos + b) % capacity, sample = m distinct uniform slots (random.sample, :53).
- * `ring` is caller-owned device memory of eco_replay_compact_bytes(); it also holds the current state of
- * each of the env's `batch` episodes (the s of their next transition).  Requires |J s| < 2^15 (reported
- * through eco_check_errors) and max_steps < 2^15. */
+/* ReplayBuffer (dqn/utils.py:28-83) of MaxCut (OptimisationTarget.CUT) transitions stored as integer env
+ * state: ONE state per transition -- per vertex a u32 {spin sign | time-since-flip count | local field
+ * (J s)_v as int16} -- plus four float64 observation scalars for s and for s' and graph id / action /
+ * reward / done: 4N + 80 bytes per transition.  s' is rebuilt on sample from s, the action and the graph
+ * (the env's step), and both states' feature rows are rebuilt with the env's own observation arithmetic
+ * (spinsystem.py:486-535), bit-exactly.  Same ReplayBuffer semantics: the newest `capacity` transitions
+ * are held, sample = m distinct uniform ones (random.sample, :53).  `pushed` counts the transitions added
+ * over the buffer's life (the k-th lives in slot k % (capacity + batch)); push writes each episode's s'
+ * straight into the slot of its next transition, so `ring` (caller-owned device memory of
+ * eco_replay_compact_bytes()) has `batch` slots more than `capacity`.  Requires |J s| < 2^15 (reported
+ * through eco_check_errors), max_steps < 2^15 and n_spins <= ECO_COMPACT_MAX_SPINS. */
+#define ECO_COMPACT_MAX_SPINS 8192
 size_t eco_replay_compact_bytes(int32_t n_spins, int32_t capacity, int32_t batch);
-/* After env reset (all episodes, or those with mask != 0): record their current states. */
+/* After env reset (all episodes, or those with mask != 0): record their states as the s of the transitions
+ * pushed + e. */
 int eco_replay_compact_snapshot(const eco_env_config *cfg, const void *env_state, int32_t batch, void *ring,
-                                int32_t capacity, const uint8_t *mask, eco_stream_t stream);
-/* After env step: ReplayBuffer.add of (s, a, r, s', done) for every episode (dqn.py:298-304); s' becomes the
- * episode's current state.  graph ids come from the env state. */
+                                int32_t capacity, int64_t pushed, const uint8_t *mask, eco_stream_t stream);
+/* After env step: ReplayBuffer.add of (s, a, r, s', done) for every episode (dqn.py:298-304) as transitions
+ * pushed .. pushed + batch - 1; graph ids come from the env state. */
 int eco_replay_compact_push(const eco_env_config *cfg, const void *env_state, int32_t batch, void *ring,
-                            int32_t capacity, int32_t pos, const int32_t *actions, const double *rewards,
+                            int32_t capacity, int64_t pushed, const int32_t *actions, const double *rewards,
                             const uint8_t *dones, eco_stream_t stream);
-/* ReplayBuffer.sample: m distinct slots of the first `size` (keyed like eco_replay_sample) expanded into
+/* ReplayBuffer.sample: m distinct transitions of the newest `size` (keyed like eco_replay_sample: the same
+ * keys pick the same transitions as the fp32 feature ring filled by the same pushes) expanded into
  * node-feature rows xs / xn [m][N][ECO_OBS_X_STRIDE(n_obs)] plus graph ids, actions, rewards, dones.
  * env_state / env_batch: the env the ring was filled from (its f64 time table); gs: its graph set. */
 int eco_replay_compact_sample(const eco_env_config *cfg, const void *env_state, const eco_graph_set *gs,
-                              int32_t env_batch, const void *ring, int32_t capacity, int32_t size, int32_t m,
-                              uint64_t seed, uint64_t counter, float *xs, float *xn, int32_t *graph_ids,
+                              int32_t env_batch, const void *ring, int32_t capacity, int32_t size, int64_t pushed,
+                              int32_t m, uint64_t seed, uint64_t counter, float *xs, float *xn, int32_t *graph_ids,
                               int32_t *actions, float *rewards, float *dones, eco_stream_t stream);
 
 /* Device-side errors (bad action, invalid graph, non-signed injected spins) are
