@@ -29,9 +29,15 @@
 
 namespace eco {
 
-constexpr int SH_EPS = 4;              // episodes per slice
+#ifndef SH_EPS_X
+#define SH_EPS_X 4
+#endif
+#ifndef SH_NW_X
+#define SH_NW_X 16
+#endif
+constexpr int SH_EPS = SH_EPS_X;       // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per wave tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
-constexpr int SH_NW = 16;              // waves per workgroup (one workgroup per CU: <= 128 VGPRs)
+constexpr int SH_NW = SH_NW_X;         // waves per workgroup (one workgroup per CU: <= 128 VGPRs at 16)
 constexpr int SH_GROUPS = 8;           // episode-slice groups: one per XCD (block b -> group b % 8)
 constexpr int SH_PART = SH_EPS * 64;   // floats of one slice's column-sum partial
 
