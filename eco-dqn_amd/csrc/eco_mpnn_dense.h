@@ -371,6 +371,19 @@ __device__ __forceinline__ void dense_adjacency(const MpnnArgs& a, uint32_t* ADJ
   if (built) __syncthreads();
 }
 
+// d[nt] = W[16 nt + .][0..7] . x of the lane's tile (the 8-input Linears: W0, Wx) on v_mfma_f32_16x16x4_f32,
+// in the node-operand layout: A = W (lane: output feature 16 nt + (l & 15), input k = l >> 4 | 4 + (l >> 4)),
+// B = x (input k, node l & 15) = this lane's xk0 / xk1.  f32 products; the forward and the backward's
+// recomputation of Z share this expression (identical ReLU decisions).  EXEC all ones.
+__device__ __forceinline__ void lin8(f32x4 (&d)[4], const float* W, float xk0, float xk1, int lane) {
+  const float* wl = W + (lane & 15) * 8 + (lane >> 4);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    d[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[nt * 128], xk0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    d[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[nt * 128 + 4], xk1, d[nt], 0, 0, 0);
+  }
+}
+
 // LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
 //      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
 //      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
@@ -403,19 +416,19 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const int s4 = lane >> 4;
   const int c16 = lane & 15;
 
-  // plane-mapped role (phases A-C): row j = 64 (w & 3) + lane, features 16 (w >> 2) .. +15
-  const int pj = 64 * (w & 3) + lane;
-  const int pft = w >> 2;
-  const bool pj_live = pj < KP;
-  const bool pj_valid = pj < rows_valid;
-  float4 xa = zero4(), xb = zero4();
-  if (pj_valid) {
-    xa = f4(a.x + (R0 + pj) * 8);
-    xb = f4(a.x + (R0 + pj) * 8 + 4);
+  // this lane's node (tile w, row w * 16 + c16) and its features k = s4, 4 + s4: the B operand of the
+  // 8-input Linears (lin8), loaded before the staging so their latency overlaps it
+  const bool has_tile = w < ntiles;
+  const int r = w * 16 + c16;
+  const bool valid = has_tile && r < rows_valid;
+  float xk0 = 0.f, xk1 = 0.f;
+  if (valid) {
+    xk0 = a.x[(R0 + r) * 8 + s4];
+    xk1 = a.x[(R0 + r) * 8 + 4 + s4];
   }
-  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree, zeroed bitmask ----
+  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree, zeroed pad rows ----
   glds_frags<NW>(WP, PB + BF_WF, 24, w, lane);
-  for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
+  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
   for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
     const int gid = a.gids[blk * a.gpb + gl];
     GB[gl] = a.gs.edge_base[gid];
@@ -423,10 +436,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   }
   __syncthreads();
   ECO_TS(1);
-  // this lane's node and its k-chunk range; its adjacency bits in registers
-  const bool has_tile = w < ntiles;
-  const int r = w * 16 + c16;
-  const bool valid = has_tile && r < rows_valid;
+  // this lane's k-chunk range; its adjacency bits in registers
   const int rr = min(r, rows_pad - 1);
   const RowInfo ri = row_info(RI, rr);
   const float nf = (float)ri.norm;
@@ -435,23 +445,23 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
   uint32_t adjb[4];
   dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
+  // plane rows [rows_pad, KP) are read (as zeros) by the last k-chunk; no tile writes them
+  for (int i = threadIdx.x; i < (KP - rows_pad) * 3 * 4 * 4; i += NT) {
+    const int k = i & 3, ft = (i >> 2) & 3, p = (i >> 4) % 3, j = rows_pad + (i >> 4) / 3;
+    *reinterpret_cast<uint2*>(PL + p * DN_PLANE + plane_off(ft, j, k)) = make_uint2(0u, 0u);
+  }
+  auto wa_of = [&](int c) { return f4(P + PK_WA + 16 * c + 4 * s4); };  // w_a of features 16c + 4 s4 .. +3
 
-  // ---- phase A: Z[j][f] = Wx[f] . x_j (weights uniform over the wave); U = relu(Z + w_a) planes ----
-  auto zval = [&](int f) {  // the CSR path's phase-A expression
-    const float* wx = P + PK_WX + f * 8;
-    return wx[0] * xa.x + wx[1] * xa.y + wx[2] * xa.z + wx[3] * xa.w + wx[4] * xb.x + wx[5] * xb.y + wx[6] * xb.z +
-           wx[7] * xb.w;
-  };
-  if (pj_live) {
+  // ---- phase A: Z = Wx . x (f32 MFMA per tile); U = relu(Z + w_a) planes ----
+  if (has_tile) {
+    f32x4 z[4];
+    lin8(z, P + PK_WX, xk0, xk1, lane);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float u[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int f = 16 * pft + 4 * k + i;
-        u[i] = pj_valid ? relu(fmaf(1.f, P[PK_WA + f], zval(f))) : 0.f;
-      }
-      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    for (int c = 0; c < 4; ++c) {
+      const float4 wa = wa_of(c);
+      plane_store4(PL, c, r, s4, valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
+                                                     relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
+                                       : zero4());
     }
   }
   glds_wait();  // Wf fragments
@@ -464,16 +474,15 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   for (int ft = 0; ft < 4; ++ft) ea[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (has_tile) dense_agg<1>(ea, PL, adjb, kc0, kc1, lane);
   __syncthreads();
-  if (pj_live) {
+  if (has_tile) {
+    f32x4 z[4];
+    lin8(z, P + PK_WX, xk0, xk1, lane);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float u[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int f = 16 * pft + 4 * k + i;
-        u[i] = pj_valid ? relu(fmaf(-1.f, P[PK_WA + f], zval(f))) : 0.f;
-      }
-      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    for (int c = 0; c < 4; ++c) {
+      const float4 wa = wa_of(c);
+      plane_store4(PL, c, r, s4, valid ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
+                                                     relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
+                                       : zero4());
     }
   }
   __syncthreads();
@@ -509,36 +518,20 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnA
   __syncthreads();  // every wave is done with the V planes and with Wf
   ECO_TS(3);
 
-  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55) as planes; the node-layout copy is read back ----
-  if (pj_live) {
+  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55), f32 MFMA per tile, kept in registers + planes ----
+  float4 hreg[4];
+  {
+    f32x4 z[4];
+    lin8(z, P + PK_W0, xk0, xk1, lane);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float u[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float* w0 = P + PK_W0 + (16 * pft + 4 * k + i) * 8;
-        const float h0 = w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
-                         w0[6] * xb.z + w0[7] * xb.w;
-        u[i] = pj_valid ? relu(h0) : 0.f;
-      }
-      plane_store4(PL, pft, pj, k, make_float4(u[0], u[1], u[2], u[3]));
+    for (int c = 0; c < 4; ++c) {
+      hreg[c] = valid ? relu4(z[c]) : zero4();
+      if (has_tile) plane_store4(PL, c, r, s4, hreg[c]);
+      if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
     }
   }
-  __syncthreads();
-  float4 hreg[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {  // p1 + p2 + p3 reproduces the f32 value exactly
-    const int o = plane_off(c, rr, s4);
-    const uint2 u1 = *reinterpret_cast<const uint2*>(PL + o);
-    const uint2 u2 = *reinterpret_cast<const uint2*>(PL + DN_PLANE + o);
-    const uint2 u3 = *reinterpret_cast<const uint2*>(PL + 2 * DN_PLANE + o);
-    auto lo = [](uint32_t v) { return __uint_as_float(v << 16); };
-    auto hi = [](uint32_t v) { return __uint_as_float(v & 0xFFFF0000u); };
-    hreg[c] = make_float4(lo(u1.x) + lo(u2.x) + lo(u3.x), hi(u1.x) + hi(u2.x) + hi(u3.x),
-                          lo(u1.y) + lo(u2.y) + lo(u3.y), hi(u1.y) + hi(u2.y) + hi(u3.y));
-    if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
-  }
   if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H0, pos_mask(hreg));
+  __syncthreads();
   ECO_TS(4);
 
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
@@ -907,20 +900,31 @@ __global__ __launch_bounds__(64 * NW, 1) void mpnn_backward_dense_kernel(MpnnArg
         dense_agg<1>(gp, PL, adjb[ti], kc0[ti], kc1[ti], lane);
         dense_agg<2>(gm, PL, adjb[ti], kc0[ti], kc1[ti], lane);
       }
-      float4 x0 = zero4(), x1 = zero4();
+      float xk0 = 0.f, xk1 = 0.f;
       if (valid[ti]) {
-        x0 = f4(a.x + (R0 + rw[ti]) * 8);
-        x1 = f4(a.x + (R0 + rw[ti]) * 8 + 4);
+        xk0 = a.x[(R0 + rw[ti]) * 8 + s4];
+        xk1 = a.x[(R0 + rw[ti]) * 8 + 4 + s4];
       }
+      f32x4 zz[4];
+      lin8(zz, P + PK_WX, xk0, xk1, lane);  // Z exactly as the forward computed it
+#ifdef ECO_DBG_VALU_Z
+      {
+        float4 x0 = zero4(), x1 = zero4();
+        if (valid[ti]) { x0 = f4(a.x + (R0 + rw[ti]) * 8); x1 = f4(a.x + (R0 + rw[ti]) * 8 + 4); }
+        for (int c = 0; c < 4; ++c) for (int i = 0; i < 4; ++i) {
+          const int f = 16 * c + 4 * s4 + i;
+          const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
+          zz[c][i] = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
+        }
+      }
+#endif
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float dz4[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int f = 16 * c + 4 * s4 + i;
-          const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
-          const float z = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y +
-                          w1.z * x1.z + w1.w * x1.w;
+          const float z = zz[c][i];
           const float wa = P[PK_WA + f];
           const float tp = fmaf(1.f, wa, z) > 0.f ? gp[c][i] : 0.f;
           const float tm = fmaf(-1.f, wa, z) > 0.f ? gm[c][i] : 0.f;

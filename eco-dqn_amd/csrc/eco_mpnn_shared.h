@@ -35,6 +35,10 @@ namespace eco {
 #ifndef SH_NW_X
 #define SH_NW_X 16
 #endif
+#ifndef SH_GRP_X
+#define SH_GRP_X 4
+#endif
+constexpr int SH_GRP = SH_GRP_X;       // edges per node gathered per group (row loads in flight per lane: 4 x SH_GRP)
 constexpr int SH_EPS = SH_EPS_X;       // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per wave tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
 constexpr int SH_NW = SH_NW_X;         // waves per workgroup (one workgroup per CU: <= 128 VGPRs at 16)
@@ -68,14 +72,14 @@ inline int shared_grid() {  // persistent workgroups: one per CU, a multiple of 
   return g;
 }
 
-// MD: row slots per tile in the edge table = N (the largest possible degree of a simple graph): the
-// table is sized without a device -> host read of max_deg.
+// MD: row slots per tile in the edge table = N + SH_GRP (the largest possible degree of a simple graph,
+// rounded up to whole groups): the table is sized without a device -> host read of max_deg.
 inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
   const size_t nlb = shared_grid() / SH_GROUPS, nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   (void)nlb;
   return (4 * ((size_t)N + 1) * Epad * 64 + (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N +
-          nt * (2 * SH_NPT + 1) + nt * (size_t)N * SH_NPT + 4 * SH_GROUPS) * sizeof(float);
+          nt * (2 * SH_NPT + 1) + nt * ((size_t)N + SH_GRP) * SH_NPT + 4 * SH_GROUPS) * sizeof(float);
 }
 
 inline SharedBufs shared_carve(float* base, int N, int B) {
@@ -84,7 +88,7 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.Epad = sb.S * SH_EPS;
   sb.nlb = shared_grid() / SH_GROUPS;
   sb.ntiles = (N + SH_NPT - 1) / SH_NPT;
-  sb.MD = N;
+  sb.MD = N + SH_GRP;
   const size_t T1 = ((size_t)N + 1) * sb.Epad * 64;
   sb.U = base;
   sb.V = sb.U + T1;
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
   int ml = len;
   for (int o = 1; o < SH_NPT; o <<= 1) ml = max(ml, __shfl_xor(ml, o, 64));  // the tile's 4 slots are lanes 4t'..
   uint32_t* et = sb.et + (size_t)t * sb.MD * SH_NPT;
-  const int ml4 = (ml + 3) & ~3;
+  const int ml4 = (ml + SH_GRP - 1) / SH_GRP * SH_GRP;
   for (int q = 0; q < ml4; ++q) et[q * SH_NPT + k] = q < len ? eg[rp[n] + q] : (uint32_t)N;  // pad: col N, w 0
   if (k == 0) sb.tinfo[(size_t)sb.ntiles * 2 * SH_NPT + t] = ml4;
 }
@@ -292,26 +296,32 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
       float4 acc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[c] = zero4();
-      uint32_t ex[4], nx[4];
-      if (ml > 0) {
+      uint32_t ex[SH_GRP], nx[SH_GRP];
+#ifdef SH_PROBE_NOGATHER
+      const int mlg = 0;
+      acc[0] = f4(Ub + (size_t)n * ld + co);  // probe: no gather
+#else
+      const int mlg = ml;
+#endif
+      if (mlg > 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ex[k] = et[k * SH_NPT];
+        for (int k = 0; k < SH_GRP; ++k) ex[k] = et[k * SH_NPT];
       }
-      for (int q = 0; q < ml; q += 4) {
-        if (q + 4 < ml) {
+      for (int q = 0; q < mlg; q += SH_GRP) {
+        if (q + SH_GRP < mlg) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) nx[k] = et[(q + 4 + k) * SH_NPT];  // next group's edge words
+          for (int k = 0; k < SH_GRP; ++k) nx[k] = et[(q + SH_GRP + k) * SH_NPT];  // next group's edge words
         }
-        float4 r[4][4];
+        float4 r[SH_GRP][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SH_GRP; ++k) {
           const int wv = edge_w(ex[k]);
           const float* src = (PHASE == 0 && wv < 0 ? sb.V : Ub) + (size_t)edge_col(ex[k]) * ld + co;
 #pragma unroll
           for (int c = 0; c < 4; ++c) r[k][c] = f4(src + c * cs);
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SH_GRP; ++k) {
           const float fw = PHASE == 0 ? 1.f : (float)edge_w(ex[k]);  // padding: zero row
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
@@ -320,7 +330,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
           }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ex[k] = nx[k];
+        for (int k = 0; k < SH_GRP; ++k) ex[k] = nx[k];
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -339,6 +349,16 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
           for (int nt = 0; nt < 4; ++nt) st4_nt(sb.EB + ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
         }
       } else {
+#ifdef SH_PROBE_NOLIN
+        if (PHASE == 1) {  // probe: gather only
+          if (nvalid) {
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) st4_nt(Hn + ro + nt * cs, rvalid ? acc[nt] : zero4());
+          }
+          item = __shfl(next, 0, 64);
+          continue;
+        }
+#endif
         f32x4 d[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
