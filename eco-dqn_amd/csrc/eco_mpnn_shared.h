@@ -44,6 +44,8 @@ constexpr int SH_NPT = 16 / SH_EPS;    // nodes per wave tile: 16 MFMA rows = SH
 constexpr int SH_NW = SH_NW_X;         // waves per workgroup (one workgroup per CU: <= 128 VGPRs at 16)
 constexpr int SH_GROUPS = 8;           // episode-slice groups: one per XCD (block b -> group b % 8)
 constexpr int SH_PART = SH_EPS * 64;   // floats of one slice's column-sum partial
+constexpr int SH_CTR = 64;             // int32 stride of the work counters: one 256-B line each (counters
+                                       // sharing a line serialise at one memory channel: ~88 dequeues/us)
 
 struct SharedBufs {
   float* U;       // [N + 1][4][Epad][16] (node, feature chunk, episode, 16 features): row N is the zero row the
@@ -57,7 +59,7 @@ struct SharedBufs {
   int32_t* perm;  // [N] nodes by decreasing degree
   int32_t* tinfo; // [ntiles][SH_NPT] {node} , [ntiles][SH_NPT] {norm}, [ntiles] {max row length}
   uint32_t* et;   // [ntiles][MD][SH_NPT] interleaved edge words (edge q of tile node k at q * SH_NPT + k)
-  int32_t* ctr;   // [3 launches][SH_GROUPS] work counters (zeroed per forward)
+  int32_t* ctr;   // [4 launches][SH_GROUPS][SH_CTR] work counters, 256-B aligned (zeroed per forward)
   int Epad, S, nlb, ntiles, MD;
 };
 
@@ -79,7 +81,7 @@ inline size_t shared_ws_bytes(int N, int B) {
   const size_t nlb = shared_grid() / SH_GROUPS, nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   (void)nlb;
   return (4 * ((size_t)N + 1) * Epad * 64 + (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N +
-          nt * (2 * SH_NPT + 1) + nt * ((size_t)N + SH_GRP) * SH_NPT + 4 * SH_GROUPS) * sizeof(float);
+          nt * (2 * SH_NPT + 1) + nt * ((size_t)N + SH_GRP) * SH_NPT + (4 * SH_GROUPS + 1) * SH_CTR) * sizeof(float);
 }
 
 inline SharedBufs shared_carve(float* base, int N, int B) {
@@ -100,7 +102,7 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.perm = reinterpret_cast<int32_t*>(sb.ql + (size_t)sb.Epad * N);
   sb.tinfo = sb.perm + N;
   sb.et = reinterpret_cast<uint32_t*>(sb.tinfo + (size_t)sb.ntiles * (2 * SH_NPT + 1));
-  sb.ctr = reinterpret_cast<int32_t*>(sb.et + (size_t)sb.ntiles * sb.MD * SH_NPT);
+  sb.ctr = reinterpret_cast<int32_t*>(((uintptr_t)(sb.et + (size_t)sb.ntiles * sb.MD * SH_NPT) + 255) & ~(uintptr_t)255);
   return sb;
 }
 
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
   const int gid = a.gids[0];
   const int grp = blockIdx.x % SH_GROUPS;  // the XCD's label (round-robin placement; speed only)
   const int n_slices = (sb.S - grp + SH_GROUPS - 1) / SH_GROUPS;  // slices grp, grp + 8, ...
-  int32_t* ctr = sb.ctr + (PHASE == 0 ? 0 : layer + 1) * SH_GROUPS + grp;
+  int32_t* ctr = sb.ctr + ((PHASE == 0 ? 0 : layer + 1) * SH_GROUPS + grp) * SH_CTR;
   const float* P = a.P;
   const float md = PHASE == 0 ? (float)(a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : a.gs.max_deg[gid]) : 1.f;
   // [node][chunk c][episode][16]: chunk c of the 4 slice episodes of a node is one 256-B run, so each
@@ -505,7 +507,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   shared_perm_kernel<<<(a.N + 255) / 256, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.ntiles * SH_NPT + 255) / 256, 256, 0, st>>>(a, sb);
   shared_prep_kernel<<<dim3((a.N + 1 + 15) / 16, (sb.Epad + 15) / 16), 256, 0, st>>>(a, sb);
-  if (hipMemsetAsync(sb.ctr, 0, 4 * SH_GROUPS * sizeof(int32_t), st) != hipSuccess)
+  if (hipMemsetAsync(sb.ctr, 0, 4 * SH_GROUPS * SH_CTR * sizeof(int32_t), st) != hipSuccess)
     return fail(ECO_ERR_HIP, "memset failed");
   const int grid = shared_grid();
   const size_t lds_edge = 24 * BF_FRAG * 2, lds_layer = 96 * BF_FRAG * 2,
