@@ -48,12 +48,14 @@ constexpr int SH_CTR = 64;             // int32 stride of the work counters: one
                                        // sharing a line serialise at one memory channel: ~88 dequeues/us)
 
 struct SharedBufs {
-  float* U;       // [N + 1][4][Epad][16] (node, feature chunk, episode, 16 features): row N is the zero row the
-                  // padded edge-table slots point at
+  float* U;       // [S][N + 1][4][SH_EPS][16] (slice, node, feature chunk, episode, 16 features): SLICE-major, so
+                  // the rows a slice's gathers touch are one contiguous 2 MB block (a node-major [node][4][Epad][16]
+                  // put them 64 KB apart -- one L2 set -- and the L2 hit rate was 31 %); row N of every slice is the zero
+                  // row the padded edge-table slots point at
   float* V;       // (graphs with negative weights only)
   float* HA;
   float* HB;
-  float* EB;      // [N][4][Epad][16]
+  float* EB;      // as U
   float* part;    // [S][ntiles][SH_EPS][64] column-sum partials of h3, one per wave tile
   float* ql;      // [Epad][N] Wr[64:] . h3
   int32_t* perm;  // [N] nodes by decreasing degree
@@ -80,7 +82,7 @@ inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
   const size_t nlb = shared_grid() / SH_GROUPS, nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   (void)nlb;
-  return (4 * ((size_t)N + 1) * Epad * 64 + (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N +
+  return (5 * ((size_t)N + 1) * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N +
           nt * (2 * SH_NPT + 1) + nt * ((size_t)N + SH_GRP) * SH_NPT + (4 * SH_GROUPS + 1) * SH_CTR) * sizeof(float);
 }
 
@@ -97,13 +99,20 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.HA = sb.V + T1;
   sb.HB = sb.HA + T1;
   sb.EB = sb.HB + T1;
-  sb.part = sb.EB + (size_t)N * sb.Epad * 64;
+  sb.part = sb.EB + T1;
   sb.ql = sb.part + (size_t)sb.S * sb.ntiles * SH_PART;
   sb.perm = reinterpret_cast<int32_t*>(sb.ql + (size_t)sb.Epad * N);
   sb.tinfo = sb.perm + N;
   sb.et = reinterpret_cast<uint32_t*>(sb.tinfo + (size_t)sb.ntiles * (2 * SH_NPT + 1));
   sb.ctr = reinterpret_cast<int32_t*>(((uintptr_t)(sb.et + (size_t)sb.ntiles * sb.MD * SH_NPT) + 255) & ~(uintptr_t)255);
   return sb;
+}
+
+// this wave's XCD (0..7): speed only -- the work-counter protocol is correct for any placement
+__device__ __forceinline__ int xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return (int)(x & 7u);
 }
 
 // streaming (non-temporal) row access: the layer's own e rows and its output rows are touched once, and
@@ -116,6 +125,19 @@ __device__ __forceinline__ float4 f4_nt(const float* p) {
 __device__ __forceinline__ void st4_nt(float* p, float4 x) {
   typedef float v4 __attribute__((ext_vector_type(4)));
   __builtin_nontemporal_store(v4{x.x, x.y, x.z, x.w}, reinterpret_cast<v4*>(p));
+}
+
+// output rows of a layer launch (e, h'): read by the NEXT launch only.  SH_SC1_STORE: sc1 stores, which drop
+// the line from this XCD's L2 instead of keeping it beside the slice being gathered.
+__device__ __forceinline__ void st4_out(float* base, size_t off, float4 x) {  // base: wave-uniform
+#ifdef SH_SC1_STORE
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(u4{__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z),
+                                            __float_as_uint(x.w)}, r, (int)(off * 4), 0, 16);
+#else
+  st4_nt(base + off, x);
+#endif
 }
 
 // mm_bf3 over LDS fragments with one output tile's fragments in flight at a time (the shared-graph layer
@@ -181,23 +203,26 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
   if (k == 0) sb.tinfo[(size_t)sb.ntiles * 2 * SH_NPT + t] = ml4;
 }
 
-// U (, V) and h0 for a block of 16 nodes x 16 episodes: the x rows are staged in LDS from 16 contiguous
-// 512-B runs (one per episode), each thread computes one (node, episode) row into an LDS image laid out
-// like the buffers, and the block stores every (node, chunk) run of 16 episodes (1 KB) with consecutive
-// lanes on consecutive 16 B.  Weights staged in LDS.  Same arithmetic as the phase-A / phase-C expressions
-// of the dense kernel; rows of padding episodes and the sentinel node N are zero.  V only for graphs with
-// negative weights (lower bound < 0).
+// U (, V) and h0 for a block of 64 nodes x the SH_EPS episodes of one slice: the x rows are staged in LDS
+// (one 2-KB run per episode), each thread computes one (node, episode) row into an LDS image laid out exactly
+// like the slice's block of the buffer ([node][chunk][episode][16], one 4-float pad per node), and the block
+// stores the image as one contiguous 64-KB run (consecutive lanes on consecutive 16 B).  Weights staged in
+// LDS.  Same arithmetic as the phase-A / phase-C expressions of the dense kernel's per-row form; rows of
+// padding episodes and the sentinel node N are zero.  V only for graphs with negative weights.
+constexpr int SHP_NODES = 64;
+constexpr int SHP_ROW = 4 * SH_EPS * 16 + 4;  // floats per node of the LDS image (+4: rotates the banks)
+static_assert(SHP_NODES * SH_EPS == 256, "one row per thread");
 __global__ __launch_bounds__(256) void shared_prep_kernel(MpnnArgs a, SharedBufs sb) {
-  __shared__ float WS[1088];                                      // PK_W0 [64][8] | PK_WX [64][8] | PK_WA [64]
-  __shared__ __attribute__((aligned(16))) float XS[16][16][8];     // [episode][node][8]
-  __shared__ __attribute__((aligned(16))) float RB[16][4][16][20]; // [node][chunk][episode][16 (+4 pad)]
+  __shared__ float WS[1088];                                                // PK_W0 | PK_WX | PK_WA
+  __shared__ __attribute__((aligned(16))) float XS[SH_EPS][SHP_NODES][8];  // [episode][node][8]
+  __shared__ __attribute__((aligned(16))) float RB[SHP_NODES * SHP_ROW];    // the image
   const int t = threadIdx.x;
-  const int n0 = blockIdx.x * 16, e0 = blockIdx.y * 16;
+  const int n0 = blockIdx.x * SHP_NODES, s = blockIdx.y;
   const int N = a.N;
   for (int i = t; i < 1088; i += 256) WS[i] = a.P[i];
   {
-    const int el = t >> 4, nl = t & 15;
-    const int e = e0 + el, n = n0 + nl;
+    const int el = t / SHP_NODES, nl = t % SHP_NODES;  // consecutive threads: consecutive nodes of one episode
+    const int e = s * SH_EPS + el, n = n0 + nl;
     const bool ok = e < a.B && n < N;
     float4* xd = reinterpret_cast<float4*>(&XS[el][nl][0]);
     xd[0] = ok ? f4(a.x + ((size_t)e * N + n) * 8) : zero4();
@@ -205,14 +230,16 @@ __global__ __launch_bounds__(256) void shared_prep_kernel(MpnnArgs a, SharedBufs
   }
   __syncthreads();
   const bool neg = a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0;
-  const int nl = t >> 4, el = t & 15;  // compute role: row (node n0 + nl, episode e0 + el)
-  const bool valid = e0 + el < a.B && n0 + nl < N;
+  const int nl = t / SH_EPS, el = t % SH_EPS;  // compute role: row (node n0 + nl, episode s * SH_EPS + el)
+  const bool valid = s * SH_EPS + el < a.B && n0 + nl < N;
   const float4 xa = *reinterpret_cast<const float4*>(&XS[el][nl][0]);
   const float4 xb = *reinterpret_cast<const float4*>(&XS[el][nl][4]);
-  const size_t cs = (size_t)sb.Epad * 16;
+  const size_t ss = ((size_t)N + 1) * 4 * SH_EPS * 16;  // floats per slice
+  const int n_hi = min(SHP_NODES, N + 1 - n0);          // nodes of this block (node N: the zero row)
   for (int which = 0; which < 3; ++which) {  // 0: U, 1: V, 2: h0
     if (which == 1 && !neg) continue;
     float* dst = which == 0 ? sb.U : which == 1 ? sb.V : sb.HA;
+    float* row = RB + nl * SHP_ROW + el * 16;
 #pragma unroll 4
     for (int f = 0; f < 64; ++f) {
       float val;
@@ -226,17 +253,16 @@ __global__ __launch_bounds__(256) void shared_prep_kernel(MpnnArgs a, SharedBufs
         val = relu(w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
                    w0[6] * xb.z + w0[7] * xb.w);
       }
-      RB[nl][f >> 4][el][f & 15] = valid ? val : 0.f;
+      row[(f >> 4) * (SH_EPS * 16) + (f & 15)] = valid ? val : 0.f;
     }
     __syncthreads();
-    // 16 nodes x 4 chunks x 16 episodes x 4 float4: thread i -> run (node, chunk), episode, float4
-    for (int i = t; i < 16 * 4 * 16 * 4; i += 256) {
-      const int j4 = i & 3, e_l = (i >> 2) & 15, c = (i >> 6) & 3, n_l = i >> 8;
-      const int n = n0 + n_l;
-      if (n > N) continue;
-      float* o = dst + ((size_t)n * 4 + c) * cs + (size_t)(e0 + e_l) * 16 + 4 * j4;
-      if (e0 + e_l < sb.Epad) st4(o, *reinterpret_cast<const float4*>(&RB[n_l][c][e_l][4 * j4]));
-      if (which == 2 && n == N && e0 + e_l < sb.Epad) st4(sb.HB + ((size_t)n * 4 + c) * cs + (size_t)(e0 + e_l) * 16 + 4 * j4, zero4());
+    // the image -> the slice's rows n0 .. n0 + n_hi - 1: one contiguous run
+    float* o = dst + (size_t)s * ss + (size_t)n0 * (4 * SH_EPS * 16);
+    for (int k = t; k < n_hi * SH_EPS * 16; k += 256) {  // float4 k of the run
+      const int nd = k / (SH_EPS * 16), q = k % (SH_EPS * 16);
+      const float4 v = *reinterpret_cast<const float4*>(&RB[nd * SHP_ROW + 4 * q]);
+      st4(o + 4 * (size_t)k, v);
+      if (which == 2 && n0 + nd == N) st4(sb.HB + (size_t)s * ss + (size_t)N * (4 * SH_EPS * 16) + 4 * q, zero4());
     }
     __syncthreads();
   }
@@ -260,15 +286,18 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
   else glds_frags<SH_NW>(WL, PB + BF_LAYER + layer * BF_LAYER_STRIDE, 96, w, lane);
   const int N = a.N;
   const int gid = a.gids[0];
-  const int grp = blockIdx.x % SH_GROUPS;  // the XCD's label (round-robin placement; speed only)
-  const int n_slices = (sb.S - grp + SH_GROUPS - 1) / SH_GROUPS;  // slices grp, grp + 8, ...
-  int32_t* ctr = sb.ctr + ((PHASE == 0 ? 0 : layer + 1) * SH_GROUPS + grp) * SH_CTR;
+#ifdef SH_GROUP_BY_BLOCK
+  const int home = blockIdx.x % SH_GROUPS;  // round-robin placement assumed
+#else
+  const int home = xcc_id();  // this CU's XCD: its waves share one counter (and one L2) whatever the placement
+#endif
   const float* P = a.P;
   const float md = PHASE == 0 ? (float)(a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : a.gs.max_deg[gid]) : 1.f;
-  // [node][chunk c][episode][16]: chunk c of the 4 slice episodes of a node is one 256-B run, so each
+  // [slice][node][chunk c][episode][16]: chunk c of the 4 slice episodes of a node is one 256-B run, so each
   // gather instruction (fixed c, 16 rows = 4 nodes x 4 episodes) reads 4 whole 256-B runs
-  const size_t ld = (size_t)sb.Epad * 64;  // floats per node block
-  const size_t cs = (size_t)sb.Epad * 16;  // floats per feature chunk of a node block
+  const size_t ld = (size_t)SH_EPS * 64;  // floats per node block of a slice
+  const size_t cs = (size_t)SH_EPS * 16;  // floats per feature chunk of a node block
+  const size_t ss = ((size_t)N + 1) * ld;  // floats per slice
   const float* Ub = PHASE == 0 ? sb.U : Hc;
   glds_wait();
   __syncthreads();
@@ -276,6 +305,13 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
   // waves of one XCD stay within about one slice of each other whatever their speeds (a static split
   // drifted apart over many slices and the L2 held none of them); the next item is claimed while the
   // current one is computed.
+  // Every group's counter is drained by whoever gets there: the home group's first, then the others' (only
+  // their tails are left when the placement is balanced), so each tile is computed exactly once whatever
+  // the workgroup -> XCD placement.
+  for (int gi = 0; gi < SH_GROUPS; ++gi) {
+  const int grp = (home + gi) % SH_GROUPS;
+  const int n_slices = (sb.S - grp + SH_GROUPS - 1) / SH_GROUPS;  // slices grp, grp + 8, ...
+  int32_t* ctr = sb.ctr + ((PHASE == 0 ? 0 : layer + 1) * SH_GROUPS + grp) * SH_CTR;
   int item = 0;
   if (lane == 0) item = atomicAdd(ctr, 1);
   item = __shfl(item, 0, 64);
@@ -287,7 +323,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
     const int s = grp + SH_GROUPS * sl, t = item - sl * sb.ntiles;
     const int ep = s * SH_EPS + eps;
     const bool evalid = ep < a.B;
-    const size_t co = (size_t)ep * 16 + 4 * s4;  // this lane's offset inside chunk 0 of a node block
+    const size_t co = (size_t)s * ss + (size_t)eps * 16 + 4 * s4;  // slice base + this lane's offset in chunk 0
     {
       const int slot = t * SH_NPT + kn;
       const bool nvalid = slot < N;
@@ -348,7 +384,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
         mm_bf3_seq(d, acc, WL, lane);
         if (nvalid) {
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) st4_nt(sb.EB + ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
+          for (int nt = 0; nt < 4; ++nt) st4_out(sb.EB, ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
         }
       } else {
 #ifdef SH_PROBE_NOLIN
@@ -387,7 +423,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
         if (PHASE == 1) {
           if (nvalid) {
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) st4_nt(Hn + ro + nt * cs, rvalid ? relu4(hn[nt]) : zero4());
+            for (int nt = 0; nt < 4; ++nt) st4_out(Hn, ro + nt * cs, rvalid ? relu4(hn[nt]) : zero4());
           }
         } else {
           float qp = 0.f;
@@ -416,6 +452,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_layer_kernel(MpnnArgs a,
       }
     }
     item = __shfl(next, 0, 64);
+  }
   }
 }
 
@@ -506,7 +543,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   shared_perm_kernel<<<(a.N + 255) / 256, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.ntiles * SH_NPT + 255) / 256, 256, 0, st>>>(a, sb);
-  shared_prep_kernel<<<dim3((a.N + 1 + 15) / 16, (sb.Epad + 15) / 16), 256, 0, st>>>(a, sb);
+  shared_prep_kernel<<<dim3((a.N + 1 + SHP_NODES - 1) / SHP_NODES, sb.S), 256, 0, st>>>(a, sb);
   if (hipMemsetAsync(sb.ctr, 0, 4 * SH_GROUPS * SH_CTR * sizeof(int32_t), st) != hipSuccess)
     return fail(ECO_ERR_HIP, "memset failed");
   const int grid = shared_grid();
