@@ -164,19 +164,26 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
   }
 }
 
-// perm[rank] = node, nodes ranked by decreasing degree (index on ties): one thread per node
+// perm[rank] = node, nodes ranked by decreasing degree (index on ties): one thread per node, the degrees
+// staged in LDS in chunks of 2048 (each thread compares against every node: from LDS, not N global loads)
 __global__ __launch_bounds__(256) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
+  __shared__ int DG[2048];
   const int N = a.N;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int32_t* rp = a.gs.row_ptr + (size_t)a.gids[0] * (N + 1);
-  if (i >= N) return;
-  const int di = rp[i + 1] - rp[i];
+  const int di = i < N ? rp[i + 1] - rp[i] : 0;
   int r = 0;
-  for (int j = 0; j < N; ++j) {
-    const int dj = rp[j + 1] - rp[j];
-    r += (dj > di) || (dj == di && j < i);
+  for (int j0 = 0; j0 < N; j0 += 2048) {
+    const int nj = min(2048, N - j0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < nj; j += 256) DG[j] = rp[j0 + j + 1] - rp[j0 + j];
+    __syncthreads();
+    for (int j = 0; j < nj; ++j) {
+      const int dj = DG[j];
+      r += (dj > di) || (dj == di && j0 + j < i);
+    }
   }
-  sb.perm[r] = i;
+  if (i < N) sb.perm[r] = i;
 }
 
 // tile tables: thread (tile t, slot k) -> node, norm, its edge words interleaved with the tile's other
@@ -203,68 +210,52 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
   if (k == 0) sb.tinfo[(size_t)sb.ntiles * 2 * SH_NPT + t] = ml4;
 }
 
-// U (, V) and h0 for a block of 64 nodes x the SH_EPS episodes of one slice: the x rows are staged in LDS
-// (one 2-KB run per episode), each thread computes one (node, episode) row into an LDS image laid out exactly
-// like the slice's block of the buffer ([node][chunk][episode][16], one 4-float pad per node), and the block
-// stores the image as one contiguous 64-KB run (consecutive lanes on consecutive 16 B).  Weights staged in
-// LDS.  Same arithmetic as the phase-A / phase-C expressions of the dense kernel's per-row form; rows of
-// padding episodes and the sentinel node N are zero.  V only for graphs with negative weights.
-constexpr int SHP_NODES = 64;
-constexpr int SHP_ROW = 4 * SH_EPS * 16 + 4;  // floats per node of the LDS image (+4: rotates the banks)
-static_assert(SHP_NODES * SH_EPS == 256, "one row per thread");
-__global__ __launch_bounds__(256) void shared_prep_kernel(MpnnArgs a, SharedBufs sb) {
-  __shared__ float WS[1088];                                                // PK_W0 | PK_WX | PK_WA
-  __shared__ __attribute__((aligned(16))) float XS[SH_EPS][SHP_NODES][8];  // [episode][node][8]
-  __shared__ __attribute__((aligned(16))) float RB[SHP_NODES * SHP_ROW];    // the image
-  const int t = threadIdx.x;
-  const int n0 = blockIdx.x * SHP_NODES, s = blockIdx.y;
+// U (, V) and h0: one wave per tile of SH_NPT consecutive nodes x the SH_EPS episodes of one slice (the
+// layer kernels' 16-row tile, in node order), the 8-input Linears on f32 MFMA (lin8, as the dense kernels),
+// results stored straight from the MFMA layout: one float4 per lane and feature chunk, SH_NPT whole 256-B
+// runs per store instruction (full cache lines, no LDS image, no write amplification).  Rows of padding
+// episodes and the sentinel node N are zero; nodes past N are not stored.  V only for graphs with negative
+// weights.
+constexpr int SHP_WAVES = 4;
+__global__ __launch_bounds__(64 * SHP_WAVES) void shared_prep_kernel(MpnnArgs a, SharedBufs sb) {
+  const int lane = threadIdx.x & 63;
+  const int c16 = lane & 15, s4 = lane >> 4;
+  const int kn = c16 / SH_EPS, eps = c16 % SH_EPS;
   const int N = a.N;
-  for (int i = t; i < 1088; i += 256) WS[i] = a.P[i];
-  {
-    const int el = t / SHP_NODES, nl = t % SHP_NODES;  // consecutive threads: consecutive nodes of one episode
-    const int e = s * SH_EPS + el, n = n0 + nl;
-    const bool ok = e < a.B && n < N;
-    float4* xd = reinterpret_cast<float4*>(&XS[el][nl][0]);
-    xd[0] = ok ? f4(a.x + ((size_t)e * N + n) * 8) : zero4();
-    xd[1] = ok ? f4(a.x + ((size_t)e * N + n) * 8 + 4) : zero4();
+  const int ntn = (N + 1 + SH_NPT - 1) / SH_NPT;  // node tiles incl. the sentinel row
+  const int tile = blockIdx.x * SHP_WAVES + (threadIdx.x >> 6);
+  if (tile >= ntn * sb.S) return;  // wave-uniform
+  const int s = tile / ntn, n = (tile - s * ntn) * SH_NPT + kn;
+  const int e = s * SH_EPS + eps;
+  const bool valid = e < a.B && n < N;
+  float xk0 = 0.f, xk1 = 0.f;
+  if (valid) {
+    xk0 = a.x[((size_t)e * N + n) * 8 + s4];
+    xk1 = a.x[((size_t)e * N + n) * 8 + 4 + s4];
   }
-  __syncthreads();
   const bool neg = a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0;
-  const int nl = t / SH_EPS, el = t % SH_EPS;  // compute role: row (node n0 + nl, episode s * SH_EPS + el)
-  const bool valid = s * SH_EPS + el < a.B && n0 + nl < N;
-  const float4 xa = *reinterpret_cast<const float4*>(&XS[el][nl][0]);
-  const float4 xb = *reinterpret_cast<const float4*>(&XS[el][nl][4]);
-  const size_t ss = ((size_t)N + 1) * 4 * SH_EPS * 16;  // floats per slice
-  const int n_hi = min(SHP_NODES, N + 1 - n0);          // nodes of this block (node N: the zero row)
-  for (int which = 0; which < 3; ++which) {  // 0: U, 1: V, 2: h0
-    if (which == 1 && !neg) continue;
-    float* dst = which == 0 ? sb.U : which == 1 ? sb.V : sb.HA;
-    float* row = RB + nl * SHP_ROW + el * 16;
-#pragma unroll 4
-    for (int f = 0; f < 64; ++f) {
-      float val;
-      if (which < 2) {
-        const float* wx = WS + PK_WX + f * 8;
-        const float z = wx[0] * xa.x + wx[1] * xa.y + wx[2] * xa.z + wx[3] * xa.w + wx[4] * xb.x + wx[5] * xb.y +
-                        wx[6] * xb.z + wx[7] * xb.w;
-        val = relu(fmaf(which == 0 ? 1.f : -1.f, WS[PK_WA + f], z));
-      } else {
-        const float* w0 = WS + PK_W0 + f * 8;
-        val = relu(w0[0] * xa.x + w0[1] * xa.y + w0[2] * xa.z + w0[3] * xa.w + w0[4] * xb.x + w0[5] * xb.y +
-                   w0[6] * xb.z + w0[7] * xb.w);
-      }
-      row[(f >> 4) * (SH_EPS * 16) + (f & 15)] = valid ? val : 0.f;
-    }
-    __syncthreads();
-    // the image -> the slice's rows n0 .. n0 + n_hi - 1: one contiguous run
-    float* o = dst + (size_t)s * ss + (size_t)n0 * (4 * SH_EPS * 16);
-    for (int k = t; k < n_hi * SH_EPS * 16; k += 256) {  // float4 k of the run
-      const int nd = k / (SH_EPS * 16), q = k % (SH_EPS * 16);
-      const float4 v = *reinterpret_cast<const float4*>(&RB[nd * SHP_ROW + 4 * q]);
-      st4(o + 4 * (size_t)k, v);
-      if (which == 2 && n0 + nd == N) st4(sb.HB + (size_t)s * ss + (size_t)N * (4 * SH_EPS * 16) + 4 * q, zero4());
-    }
-    __syncthreads();
+  const size_t ld = (size_t)SH_EPS * 64, cs = (size_t)SH_EPS * 16;
+  const size_t ro = (size_t)s * ((size_t)N + 1) * ld + (size_t)n * ld + (size_t)eps * 16 + 4 * s4;
+  const bool st = n <= N;
+  f32x4 z[4];
+  lin8(z, a.P + PK_WX, xk0, xk1, lane);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 wa = f4(a.P + PK_WA + 16 * c + 4 * s4);
+    if (st)
+      st4_nt(sb.U + ro + c * cs, valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
+                                                     relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
+                                       : zero4());
+    if (neg && st)
+      st4_nt(sb.V + ro + c * cs, valid ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
+                                                     relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
+                                       : zero4());
+  }
+  lin8(z, a.P + PK_W0, xk0, xk1, lane);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (st) st4_nt(sb.HA + ro + c * cs, valid ? relu4(z[c]) : zero4());
+    if (n == N) st4_nt(sb.HB + ro + c * cs, zero4());  // the other ping-pong buffer's sentinel row
   }
 }
 
@@ -543,7 +534,10 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   shared_perm_kernel<<<(a.N + 255) / 256, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.ntiles * SH_NPT + 255) / 256, 256, 0, st>>>(a, sb);
-  shared_prep_kernel<<<dim3((a.N + 1 + SHP_NODES - 1) / SHP_NODES, sb.S), 256, 0, st>>>(a, sb);
+  {
+    const int ntn = (a.N + 1 + SH_NPT - 1) / SH_NPT;
+    shared_prep_kernel<<<(ntn * sb.S + SHP_WAVES - 1) / SHP_WAVES, 64 * SHP_WAVES, 0, st>>>(a, sb);
+  }
   if (hipMemsetAsync(sb.ctr, 0, 4 * SH_GROUPS * SH_CTR * sizeof(int32_t), st) != hipSuccess)
     return fail(ECO_ERR_HIP, "memset failed");
   const int grid = shared_grid();

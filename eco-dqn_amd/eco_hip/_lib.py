@@ -17,7 +17,7 @@ lib = ctypes.CDLL(LIB_PATH)
 
 # ---- status codes / enums (eco_hip.h) ----
 ECO_OK, ECO_ERR_ARG, ECO_ERR_HIP, ECO_ERR_PAST_END, ECO_ERR_BASIS, ECO_ERR_TARGET, ECO_ERR_OBSERVABLE, \
-    ECO_ERR_GRAPH = range(8)
+    ECO_ERR_GRAPH, ECO_ERR_KEY, ECO_ERR_INDEX = range(10)
 ECO_MAX_OBS = 16          # observables per env (MAIN_OBSERVABLES has 13)
 ECO_MPNN_MAX_OBS = 16     # MPNN n_obs_in limit (node-feature rows of obs_x_stride(n_obs_in) floats)
 ECO_ENV_SCALARS = 16
@@ -104,6 +104,21 @@ _SIG = {
     "eco_replay_compact_sample": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, ctypes.POINTER(GraphSet), _I, _P, _I,
                                                  _I, ctypes.c_int64, _I, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P, _P, _P, _P,
                                                  _P]),
+    "eco_per_create": (_P, [_I, ctypes.c_double, ctypes.c_double]),
+    "eco_per_destroy": (None, [_P]),
+    "eco_per_len": (_I, [_P]),
+    "eco_per_beta": (ctypes.c_double, [_P]),
+    "eco_per_full": (ctypes.c_int, [_P]),
+    "eco_per_configure_beta_anneal_time": (ctypes.c_int, [_P, ctypes.c_double]),
+    "eco_per_add": (ctypes.c_int, [_P, _I, _P]),
+    "eco_per_update_priorities": (ctypes.c_int, [_P, _I, _P, _P]),
+    "eco_per_rebalance": (ctypes.c_int, [_P]),
+    "eco_per_sample": (ctypes.c_int, [_P, _I, _P, ctypes.c_uint64, _P, _P, _P]),
+    "eco_per_sample_begin": (ctypes.c_int, [_P, _I, _P]),
+    "eco_per_sample_finish": (ctypes.c_int, [_P, _I, _P, ctypes.c_uint64, _P, _P, _P]),
+    "eco_per_heap": (ctypes.c_int, [_P, _P, _P]),
+    "eco_per_partitions": (_I, [_P, _P, _P]),
+    "eco_replay_gather": (ctypes.c_int, [ctypes.POINTER(Replay), _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "eco_last_error": (ctypes.c_char_p, []),
 }
 for _name, (_res, _args) in _SIG.items():
@@ -131,6 +146,10 @@ def check(rc):
         raise Exception(msg)
     if rc == ECO_ERR_HIP:
         raise RuntimeError(msg)
+    if rc == ECO_ERR_KEY:
+        raise KeyError(msg)
+    if rc == ECO_ERR_INDEX:
+        raise IndexError(msg)
     raise ValueError(msg)
 
 

@@ -42,7 +42,9 @@ enum {
   ECO_ERR_BASIS = 4,       /* unknown spin basis: Exception, spinsystem.py:600-606 */
   ECO_ERR_TARGET = 5,      /* unsupported optimisation target: NotImplementedError, score_solver.py:885 */
   ECO_ERR_OBSERVABLE = 6,  /* first observable != SPIN_STATE: AssertionError, spinsystem.py:116 */
-  ECO_ERR_GRAPH = 7        /* graph with no nonzero local reward (spinsystem.py:203-211) or bad CSR */
+  ECO_ERR_GRAPH = 7,       /* graph with no nonzero local reward (spinsystem.py:203-211) or bad CSR */
+  ECO_ERR_KEY = 8,         /* missing heap / buffer position: KeyError, dqn/utils.py:236,259 */
+  ECO_ERR_INDEX = 9        /* rebalance of a heap that is not full: IndexError, dqn/utils.py:196 */
 };
 
 /* ---- enums: numerically identical to src/envs/utils.py:10-66 ---- */
@@ -298,6 +300,42 @@ int eco_replay_compact_sample(const eco_env_config *cfg, const void *env_state, 
                               int32_t env_batch, const void *ring, int32_t capacity, int32_t size, int64_t pushed,
                               int32_t m, uint64_t seed, uint64_t counter, float *xs, float *xn, int32_t *graph_ids,
                               int32_t *actions, float *rewards, float *dones, eco_stream_t stream);
+
+/* PrioritisedReplayBuffer (dqn/utils.py:86-277), rank-based: the binary max-heap of (buffer position,
+ * td error) is a native HOST structure (every add / update is a sequential up-/down-heap walk) following
+ * the reference's comparisons exactly; transitions stay in HBM in an eco_replay ring at slot = buffer
+ * position - 1 and are fetched with eco_replay_gather.  Buffer positions are 1-based like the reference's.
+ * These calls are host-only (no stream, no device memory) except eco_replay_gather. */
+typedef struct eco_per eco_per;
+eco_per *eco_per_create(int32_t capacity, double alpha, double beta0);      /* __init__, :88-111 (NULL: bad capacity) */
+void eco_per_destroy(eco_per *per);
+int32_t eco_per_len(const eco_per *per);                                   /* __len__, :278 */
+double eco_per_beta(const eco_per *per);
+int eco_per_full(const eco_per *per);
+int eco_per_configure_beta_anneal_time(eco_per *per, double beta_max_at_samples);  /* :275-276 */
+/* n consecutive add() calls (:120-142); buffer_positions[n] (nullable) receives the positions written. */
+int eco_per_add(eco_per *per, int32_t n, int32_t *buffer_positions);
+/* update_priorities (:234-240) in the order given. */
+int eco_per_update_priorities(eco_per *per, int32_t n, const int32_t *buffer_positions, const double *td_errors);
+/* rebalance (:185-202); ECO_ERR_INDEX unless the heap is full. */
+int eco_per_rebalance(eco_per *per);
+/* sample (:242-273) without the gather: one rank per partition -- injected (`ranks`, the reference's
+ * np.random.randint(low, high) draws) or drawn natively from `seed` when NULL -- giving buffer_positions
+ * [batch], float32 importance weights [batch] and (nullable) ranks_out [batch].  = begin + finish; begin
+ * refreshes the partitions (:247-254) and writes their boundaries bounds[batch + 1] (nullable; partition k
+ * = ranks [bounds[k], bounds[k+1])), so a caller can draw the ranks with its own RNG before finish. */
+int eco_per_sample_begin(eco_per *per, int32_t batch, int32_t *bounds);
+int eco_per_sample_finish(eco_per *per, int32_t batch, const int64_t *ranks, uint64_t seed, int32_t *buffer_positions,
+                          float *weights, int64_t *ranks_out);
+int eco_per_sample(eco_per *per, int32_t batch, const int64_t *ranks, uint64_t seed, int32_t *buffer_positions,
+                   float *weights, int64_t *ranks_out);
+/* Heap positions 1..len: buffer position and td error of each (host arrays of eco_per_len()). */
+int eco_per_heap(const eco_per *per, int32_t *buffer_positions, double *td_errors);
+/* Current partitions: bounds [n+1] and rank probabilities [len] (both nullable); returns n. */
+int32_t eco_per_partitions(const eco_per *per, int32_t *bounds, double *probs);
+/* Gather m transitions of an eco_replay ring by explicit slot (DEVICE int32 slots[m], each < capacity). */
+int eco_replay_gather(const eco_replay *rb, int32_t m, const int32_t *slots, float *xs, float *xn, int32_t *graph_ids,
+                      int32_t *actions, float *rewards, float *dones, eco_stream_t stream);
 
 /* Device-side errors (bad action, invalid graph, non-signed injected spins) are
  * recorded in a device word by the asynchronous kernels; this synchronises
