@@ -136,6 +136,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0):
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "train", "pmc_hbm.json")
 PMC_SQ = os.path.join(REPO, "profiles", "r02", "train", "pmc_sq_dense.json")
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (~2.5 PF)
+PMC_GSET = os.path.join(REPO, "profiles", "r02", "gset_pmc", "pmc_hbm.json")
+L2_GATHER_TBS = 18.8  # MI355X_MICROARCH.md 'Indexed rows': L2-served row gathers, upper end of 16.8-18.8 TB/s
 
 
 def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
@@ -156,6 +158,17 @@ def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
     busy = (n_inf * inf["mfma_busy"] + n_trn * trn["mfma_busy"]) / (n_inf + n_trn)
     ratio = inf["issued_bf16_flop"] / (flops_per_graph * M)
     return {"mfma_busy": busy, "issued_per_algorithmic_flop": ratio, "source": os.path.relpath(PMC_SQ, REPO)}
+
+
+def pmc_gset_traffic():
+    """HBM bytes of one configs[4] forward (shared-graph prep + edge + 3 layer launches) from the committed
+    PMC summary (2 x FETCH_SIZE + WRITE_SIZE, KB = 1024 B), or None."""
+    try:
+        with open(PMC_GSET) as f:
+            k = json.load(f)["kernels"]
+        return sum(v["hbm_bytes_per_launch"] for name, v in k.items() if name.startswith("shared_"))
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def pmc_traffic(dom, B, M, n, graph="ER"):
@@ -441,6 +454,8 @@ def main():
             if args.graph == "ER":
                 out["cpu_baseline"] = cpu_refcost_baseline(n)
                 out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+                out["vs_cpu_baseline_note"] = ("GPU full train loop (act + env step + replay + 8 gradient steps) "
+                                               "over the CPU reference-cost env step alone (no network, no training)")
             out["cpu_baseline_learn_loop"] = cpu_baseline(n, train=train)
         print(json.dumps(out))
     if dist:
@@ -530,6 +545,18 @@ def inference_bench(args, world, rank, local, dev, dist):
             "best_cut_after_steps": best_cut,
             "process_group": pg,
         }
+        if args.workload == "gset":
+            # the shared-graph kernels are bound by gathering neighbour rows from L2, not by MFMA: every
+            # phase (edge + 3 layers) reads one 256-B fp32 row per edge per episode
+            gb = 4 * nnz * B * 256
+            out["roofline"]["gather"] = {
+                "bound": "l2-gather", "bytes_per_forward": gb, "achieved": gb / (fwd_ms * 1e-3) / 1e12,
+                "unit": "TB/s", "ceiling": L2_GATHER_TBS, "frac": gb / (fwd_ms * 1e-3) / 1e12 / L2_GATHER_TBS,
+                "ceiling_source": "MI355X_MICROARCH.md 'Indexed rows': rows shared by every workgroup, served "
+                                  "by the XCD's L2: 16.8-18.8 TB/s chip-wide"}
+            out["roofline"]["traffic"] = pmc_gset_traffic()
+            out["roofline"]["traffic_unit"] = "HBM bytes per forward (prep + 4 phase launches; PMC, " + \
+                os.path.relpath(PMC_GSET, REPO) + ")"
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()

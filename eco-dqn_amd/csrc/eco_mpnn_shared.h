@@ -165,18 +165,19 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
 }
 
 // perm[rank] = node, nodes ranked by decreasing degree (index on ties): one thread per node, the degrees
-// staged in LDS in chunks of 2048 (each thread compares against every node: from LDS, not N global loads)
-__global__ __launch_bounds__(256) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
+// staged in LDS in chunks of 2048 (each thread compares against every node: from LDS, not N global loads);
+// one wave per workgroup, so N / 64 CUs share the work
+__global__ __launch_bounds__(64) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
   __shared__ int DG[2048];
   const int N = a.N;
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * 64 + threadIdx.x;
   const int32_t* rp = a.gs.row_ptr + (size_t)a.gids[0] * (N + 1);
   const int di = i < N ? rp[i + 1] - rp[i] : 0;
   int r = 0;
   for (int j0 = 0; j0 < N; j0 += 2048) {
     const int nj = min(2048, N - j0);
     __syncthreads();
-    for (int j = threadIdx.x; j < nj; j += 256) DG[j] = rp[j0 + j + 1] - rp[j0 + j];
+    for (int j = threadIdx.x; j < nj; j += 64) DG[j] = rp[j0 + j + 1] - rp[j0 + j];
     __syncthreads();
     for (int j = 0; j < nj; ++j) {
       const int dj = DG[j];
@@ -532,7 +533,7 @@ __global__ __launch_bounds__(256) void shared_readout_kernel(MpnnArgs a, SharedB
 
 static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStream_t st) {
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
-  shared_perm_kernel<<<(a.N + 255) / 256, 256, 0, st>>>(a, sb);
+  shared_perm_kernel<<<(a.N + 63) / 64, 64, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.ntiles * SH_NPT + 255) / 256, 256, 0, st>>>(a, sb);
   {
     const int ntn = (a.N + 1 + SH_NPT - 1) / SH_NPT;

@@ -32,7 +32,9 @@ constexpr int LDY = 68, LDX = 132;         // padded LDS row strides
 struct WJobs {
   WJob j[MAX_JOBS];
   int n;
-  int nwg;  // workgroups (= slabs) per job, <= WG_PER_JOB
+  int nwg;  // workgroups (= slabs) per job, <= WG_PER_JOB (wgrad_kernel: every job)
+  int nwgj[MAX_JOBS];     // wgrad_bf3_kernel / reduce: workgroups (= slabs) of job j, <= WG_PER_JOB
+  int first[MAX_JOBS + 1];  // wgrad_bf3_kernel: first flat block of job j (1-D grid of first[n] blocks)
 };
 
 // One workgroup (4 waves) reduces a contiguous row range of one job: 32-row tiles of dY and
@@ -165,14 +167,17 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   constexpr int PY = 64 * WB_LD, PX = 128 * WB_LD;  // plane strides (bf16)
   __shared__ __attribute__((aligned(16))) uint16_t sY[3 * PY];
   __shared__ __attribute__((aligned(16))) uint16_t sX[3 * PX];
-  const WJob& J = jobs.j[blockIdx.y];
+  int jb = 0;
+  while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
+  const int wg = (int)blockIdx.x - jobs.first[jb], nwg = jobs.nwgj[jb];
+  const WJob& J = jobs.j[jb];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int jj = lane & 31, h = lane >> 5;
   const int K = J.K1 + J.K2;
   const int ntile = 2 * ((K + 31) / 32);
-  const int chunk = ((J.R + jobs.nwg - 1) / jobs.nwg + WROWS - 1) / WROWS * WROWS;
-  const int r0 = blockIdx.x * chunk;
+  const int chunk = ((J.R + nwg - 1) / nwg + WROWS - 1) / WROWS * WROWS;
+  const int r0 = wg * chunk;
   const int r1 = min(J.R, r0 + chunk);
   // staging roles: dY column yc of rows 8 yg .. +7; X columns xc (+ 0 / 1 x 128 units) of rows 8 xg .. +7
   const int yc = threadIdx.x & 63, yg = threadIdx.x >> 6;
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
       __syncthreads();
     }
   }
-  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x) * SLAB;
+  float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int t = w + 4 * q;
@@ -309,7 +314,7 @@ __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad)
   if (o >= J.nO || i >= K) return;
   const float* s = slabs + (size_t)blockIdx.y * SLABS_PER_JOB * SLAB + o * 128 + i;
   float acc = 0.f;
-  for (int k = 0; k < jobs.nwg; ++k) acc += s[(size_t)k * SLAB];
+  for (int k = 0; k < jobs.nwgj[blockIdx.y]; ++k) acc += s[(size_t)k * SLAB];
   grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
 }
 
@@ -707,11 +712,21 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   static const bool f32_wgrad = getenv("ECO_WGRAD_F32") != nullptr;  // A/B switch: the f32-MFMA reduction
   if (f32_wgrad) {
     J.nwg = WG_PER_JOB;
+    for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
     wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
   } else {
-    // 46 KB LDS -> 3 workgroups per CU: one resident wave of workgroups over the 256 CUs
-    J.nwg = std::min(WG_PER_JOB, 3 * 256 / n);
-    wgrad_bf3_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
+    // 46 KB LDS -> 3 workgroups per CU: one resident wave of 768 workgroups over the 256 CUs, dealt to
+    // the jobs in proportion to the bytes each reads ((64 + K) floats per row): with an equal split the
+    // K = 128 jobs (Wm, Wu) ran 1.35x longer than the mean and set the launch time
+    double tot = 0.0;
+    for (int j = 0; j < n; ++j) tot += (double)J.j[j].R * (64 + J.j[j].K1 + J.j[j].K2);
+    J.first[0] = 0;
+    for (int j = 0; j < n; ++j) {
+      const double wj = (double)J.j[j].R * (64 + J.j[j].K1 + J.j[j].K2);
+      J.nwgj[j] = std::max(2, std::min(WG_PER_JOB, (int)(3 * 256 * wj / tot + 0.5)));
+      J.first[j + 1] = J.first[j] + J.nwgj[j];
+    }
+    wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
   }
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
   colsum_kernel<<<64, 256, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
