@@ -137,7 +137,6 @@ PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "train", "pmc_hbm.json")
 PMC_SQ = os.path.join(REPO, "profiles", "r02", "train", "pmc_sq_dense.json")
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (~2.5 PF)
 PMC_GSET = os.path.join(REPO, "profiles", "r02", "gset_pmc", "pmc_hbm.json")
-L2_GATHER_TBS = 18.8  # MI355X_MICROARCH.md 'Indexed rows': L2-served row gathers, upper end of 16.8-18.8 TB/s
 
 
 def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
@@ -166,7 +165,8 @@ def pmc_gset_traffic():
     try:
         with open(PMC_GSET) as f:
             k = json.load(f)["kernels"]
-        return sum(v["hbm_bytes_per_launch"] for name, v in k.items() if name.startswith("shared_"))
+        return sum(v["hbm_bytes_per_launch"] * v["launches_per_forward"] for name, v in k.items()
+                   if name.startswith("shared_"))
     except (OSError, ValueError, KeyError):
         return None
 
@@ -546,17 +546,15 @@ def inference_bench(args, world, rank, local, dev, dist):
             "process_group": pg,
         }
         if args.workload == "gset":
-            # the shared-graph kernels are bound by gathering neighbour rows from L2, not by MFMA: every
-            # phase (edge + 3 layers) reads one 256-B fp32 row per edge per episode
-            gb = 4 * nnz * B * 256
-            out["roofline"]["gather"] = {
-                "bound": "l2-gather", "bytes_per_forward": gb, "achieved": gb / (fwd_ms * 1e-3) / 1e12,
-                "unit": "TB/s", "ceiling": L2_GATHER_TBS, "frac": gb / (fwd_ms * 1e-3) / 1e12 / L2_GATHER_TBS,
-                "ceiling_source": "MI355X_MICROARCH.md 'Indexed rows': rows shared by every workgroup, served "
-                                  "by the XCD's L2: 16.8-18.8 TB/s chip-wide"}
-            out["roofline"]["traffic"] = pmc_gset_traffic()
-            out["roofline"]["traffic_unit"] = "HBM bytes per forward (prep + 4 phase launches; PMC, " + \
+            # the shared-graph kernels stream node rows through HBM (aggregation from LDS-staged blocks,
+            # row-wise Linears): HBM bytes of one forward from the committed PMC pass, over the live time
+            tb = pmc_gset_traffic()
+            out["roofline"]["traffic"] = tb
+            out["roofline"]["traffic_unit"] = "HBM bytes per forward (prep + aggregation + Linear launches; PMC, " + \
                 os.path.relpath(PMC_GSET, REPO) + ")"
+            if tb:
+                out["roofline"]["hbm"] = {"bound": "hbm", "achieved": tb / (fwd_ms * 1e-3) / 1e9, "unit": "GB/s",
+                                          "peak": HBM_PEAK_GBS, "frac": tb / (fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()
