@@ -15,8 +15,9 @@
 // an aggregation item (s, c, e) is one contiguous N x 64 B block, and a Linear tile's rows of one chunk are
 // SH_EPS runs of 4 consecutive nodes x 64 B = 256 B.
 //
-// Phases (one launch each):
-//   prep:    U = relu(Wx.x + w_a), V = relu(Wx.x - w_a) and h0 = relu(W0.x) per node and episode
+// Phases (one launch each; U = relu(Wx.x + w_a), V = relu(Wx.x - w_a) and h0 = relu(W0.x) are never stored:
+// the aggregation launches build their blocks from the 32-B observation rows, the first update layer its
+// own rows):
 //   edge:    AG = A+.U (+ A-.V);  e = relu(Wf.[AG / deg, deg / norm.max()])   (mpnn.py:89-104, +-1 weights)
 //   layers:  AG = A.h;  m = relu(Wm.[AG / deg, e]), h' = relu(Wu.[h, m])  (mpnn.py:114-120, x3)
 //            the last layer writes no h3: it emits q_local = Wr[64:].h3 per node and episode and the
@@ -54,10 +55,8 @@ constexpr int AG_TPW = AG_TPW_X;       // aggregation tiles per wave in flight t
 constexpr int AG_UNROLL = AG_UNROLL_X; // edge words in flight per lane
 
 struct SharedBufs {
-  float* U;       // [S][4][SH_EPS][N][16]
-  float* V;       // (graphs with negative weights only)
-  float* HA;
-  float* HB;
+  float* HA;      // [S][4][SH_EPS][N][16]: h2 (h0, U and V are never stored: the aggregation launches and the
+  float* HB;      //  first update layer rebuild them from the observation rows, 32 B per node instead of 256 B)
   float* EB;
   float* AG;      // the aggregation of the current phase (raw neighbour sums, not yet divided by the degree)
   float* part;    // [S][ntiles][SH_EPS][64] column-sum partials of h3, one per Linear tile
@@ -84,7 +83,7 @@ inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
   const size_t nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   const size_t nt16 = ((size_t)N + 15) / 16, MD = (size_t)N + AG_UNROLL;
-  return (6 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + nt16 * MD * 16) *
+  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + nt16 * MD * 16) *
          sizeof(float);
 }
 
@@ -94,9 +93,7 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.Epad = sb.S * SH_EPS;
   sb.ntiles = (N + SH_NPT - 1) / SH_NPT;
   const size_t T1 = (size_t)N * sb.Epad * 64;
-  sb.U = base;
-  sb.V = sb.U + T1;
-  sb.HA = sb.V + T1;
+  sb.HA = base;
   sb.HB = sb.HA + T1;
   sb.EB = sb.HB + T1;
   sb.AG = sb.EB + T1;
@@ -154,70 +151,42 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
   }
 }
 
-// perm[rank] = node, nodes ranked by decreasing degree (index on ties): one thread per node, the degrees
-// staged in LDS in chunks of 2048 (each thread compares against every node: from LDS, not N global loads);
-// one wave per workgroup, so N / 64 CUs share the work
-__global__ __launch_bounds__(64) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
-  __shared__ int DG[2048];
+// perm[rank] = node, nodes ranked by decreasing degree (index on ties).  A workgroup ranks 64 nodes with 4
+// threads per node, each comparing against a quarter of the degrees (staged in LDS in chunks of 2048, read
+// 4 at a time); the four partial counts are summed with shuffles.
+__global__ __launch_bounds__(256) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
+  __shared__ __attribute__((aligned(16))) int DG[2048];
   const int N = a.N;
-  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int i = blockIdx.x * 64 + (threadIdx.x >> 2), part = threadIdx.x & 3;
   const int32_t* rp = a.gs.row_ptr + (size_t)a.gids[0] * (N + 1);
   const int di = i < N ? rp[i + 1] - rp[i] : 0;
   int r = 0;
   for (int j0 = 0; j0 < N; j0 += 2048) {
     const int nj = min(2048, N - j0);
     __syncthreads();
-    for (int j = threadIdx.x; j < nj; j += 64) DG[j] = rp[j0 + j + 1] - rp[j0 + j];
+    for (int j = threadIdx.x; j < 2048; j += 256) DG[j] = j < nj ? rp[j0 + j + 1] - rp[j0 + j] : -1;
     __syncthreads();
-    for (int j = 0; j < nj; ++j) {
-      const int dj = DG[j];
-      r += (dj > di) || (dj == di && j0 + j < i);
+    const int q0 = part * 512;  // this thread's quarter of the chunk, 4 degrees per LDS read
+    for (int j = q0; j < min(q0 + 512, nj); j += 4) {
+      const int4 d = *reinterpret_cast<const int4*>(&DG[j]);
+      const int jj = j0 + j;
+      r += (d.x > di) || (d.x == di && jj < i);
+      r += (d.y > di) || (d.y == di && jj + 1 < i);
+      r += (d.z > di) || (d.z == di && jj + 2 < i);
+      r += (d.w > di) || (d.w == di && jj + 3 < i);
     }
   }
-  if (i < N) sb.perm[r] = i;
+  r += __shfl_xor(r, 1, 64);
+  r += __shfl_xor(r, 2, 64);
+  if (i < N && part == 0) sb.perm[r] = i;
 }
 
-// U (, V) and h0: one wave per Linear tile (SH_NPT consecutive nodes x the SH_EPS episodes of one slice),
-// the 8-input Linears on f32 MFMA (lin8, as the dense kernels), results stored straight from the MFMA
-// layout: per store instruction SH_EPS runs of SH_NPT x 64 B.  Rows of padding episodes are zero.  V only
-// for graphs with negative weights.
-constexpr int SHP_WAVES = 4;
-__global__ __launch_bounds__(64 * SHP_WAVES) void shared_prep_kernel(MpnnArgs a, SharedBufs sb) {
-  const int lane = threadIdx.x & 63;
-  const int c16 = lane & 15, s4 = lane >> 4;
-  const int kn = c16 / SH_EPS, eps = c16 % SH_EPS;
-  const int N = a.N;
-  const int tile = blockIdx.x * SHP_WAVES + (threadIdx.x >> 6);
-  if (tile >= sb.ntiles * sb.S) return;  // wave-uniform
-  const int s = tile / sb.ntiles, n = (tile - s * sb.ntiles) * SH_NPT + kn;
-  const int e = s * SH_EPS + eps;
-  const bool valid = e < a.B && n < N;
-  float xk0 = 0.f, xk1 = 0.f;
-  if (valid) {
-    xk0 = a.x[((size_t)e * N + n) * 8 + s4];
-    xk1 = a.x[((size_t)e * N + n) * 8 + 4 + s4];
-  }
-  const bool neg = a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0;
-  const size_t ro = sh_row(N, s, eps, n, s4), cs = sh_cs(N);
-  const bool st = n < N;
-  f32x4 z[4];
-  lin8(z, a.P + PK_WX, xk0, xk1, lane);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const float4 wa = f4(a.P + PK_WA + 16 * c + 4 * s4);
-    if (st)
-      st4_nt(sb.U + ro + c * cs, valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
-                                                     relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
-                                       : zero4());
-    if (neg && st)
-      st4_nt(sb.V + ro + c * cs, valid ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
-                                                     relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
-                                       : zero4());
-  }
-  lin8(z, a.P + PK_W0, xk0, xk1, lane);
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    if (st) st4_nt(sb.HA + ro + c * cs, valid ? relu4(z[c]) : zero4());
+// chunk c (features 16c .. 16c+15) of an 8-input Linear (W0 or Wx) for the lane's node l & 15: exactly the
+// d[c] of lin8 (the same two MFMAs), so h0 / U / V rebuilt here equal those of the dense kernels' form
+__device__ __forceinline__ f32x4 lin8_chunk(const float* W, int c, float xk0, float xk1, int lane) {
+  const float* wl = W + (lane & 15) * 8 + (lane >> 4);
+  const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(wl[c * 128], xk0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(wl[c * 128 + 4], xk1, d, 0, 0, 0);
 }
 
 // aggregation tile tables: thread (tile t, slot k) -> node perm[16 t + k], its CSR row interleaved with the
@@ -253,27 +222,65 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
 // each row is summed in CSR order.
 // mode 0: weight w (+-1); +1: edges with w > 0, weight 1; -1: edges with w < 0, weight 1.  accumulate: add
 // to AG (the A- pass of the edge phase).
+// XSRC 0: the block is read from src; 1 / 2 / 3: it is BUILT from the observation rows x (32 B per node) as
+// U = relu(Wx.x + w_a) / V = relu(Wx.x - w_a) / h0 = relu(W0.x) (mpnn.py:89-104, :55) with lin8_chunk: the
+// next item's x values are what is prefetched, the Linear runs when the block is written to LDS.
 constexpr int AG_PF = (8192 + 64 * AG_NW - 1) / (64 * AG_NW);  // float4 per thread per block: 128 KB (N <= 2048)
+constexpr int AG_XT = (2048 / 16 + AG_NW - 1) / AG_NW;          // 16-node x tiles per wave (N <= 2048)
+template <int XSRC>
 __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, SharedBufs sb, const float* src,
                                                                    int mode, int accumulate, int items) {
   extern __shared__ __attribute__((aligned(16))) float4 HL[];  // [N][4]
   const int N = a.N;
   if (mode < 0 && !(a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0)) return;  // no -1 edge: A- . V = 0
   const int n4 = N * 4;
-  float4 pf[AG_PF];
+  constexpr int NPF = XSRC ? 1 : AG_PF;
+  constexpr int NXT = XSRC ? AG_XT : 1;
+  float4 pf[NPF];
+  float xk0[NXT], xk1[NXT];
+  int pc = 0;  // chunk of the prefetched item (XSRC)
+  const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
   auto load_block = [&](int it) {
-    const float* S = src + (size_t)it * N * 16;
+    if (XSRC == 0) {
+      const float* S = src + (size_t)it * N * 16;
 #pragma unroll
-    for (int u = 0; u < AG_PF; ++u) {
-      const int i = threadIdx.x + u * 64 * AG_NW;
-      pf[u] = f4_nt(S + 4 * (size_t)min(i, n4 - 1));
+      for (int u = 0; u < NPF; ++u) {
+        const int i = threadIdx.x + u * 64 * AG_NW;
+        pf[u] = f4_nt(S + 4 * (size_t)min(i, n4 - 1));
+      }
+    } else {
+      const int e = it % SH_EPS, c = (it / SH_EPS) % 4, s = it / (4 * SH_EPS);
+      const int ep = s * SH_EPS + e;
+      pc = c;
+#pragma unroll
+      for (int j = 0; j < NXT; ++j) {
+        const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
+        const bool ok = ep < a.B && n < N;
+        xk0[j] = ok ? a.x[((size_t)ep * N + n) * 8 + (ln >> 4)] : 0.f;
+        xk1[j] = ok ? a.x[((size_t)ep * N + n) * 8 + 4 + (ln >> 4)] : 0.f;
+      }
     }
   };
   auto store_block = [&]() {
+    if (XSRC == 0) {
 #pragma unroll
-    for (int u = 0; u < AG_PF; ++u) {
-      const int i = threadIdx.x + u * 64 * AG_NW;
-      if (i < n4) HL[i] = pf[u];
+      for (int u = 0; u < NPF; ++u) {
+        const int i = threadIdx.x + u * 64 * AG_NW;
+        if (i < n4) HL[i] = pf[u];
+      }
+    } else {
+      const float4 wa = f4(a.P + PK_WA + 16 * pc + 4 * (ln >> 4));
+#pragma unroll
+      for (int j = 0; j < NXT; ++j) {
+        const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
+        if ((wv_ + j * AG_NW) * 16 >= N) break;  // wave-uniform: MFMAs below run with EXEC all ones
+        const f32x4 z = lin8_chunk(a.P + (XSRC == 3 ? PK_W0 : PK_WX), pc, xk0[j], xk1[j], ln);
+        const float sg = XSRC == 2 ? -1.f : 1.f;
+        float4 v = XSRC == 3 ? relu4(z)
+                             : make_float4(relu(fmaf(sg, wa.x, z[0])), relu(fmaf(sg, wa.y, z[1])),
+                                           relu(fmaf(sg, wa.z, z[2])), relu(fmaf(sg, wa.w, z[3])));
+        if (n < N) HL[n * 4 + (ln >> 4)] = v;  // padding episodes (x = 0) only ever reach their own rows
+      }
     }
   };
   int item = blockIdx.x;
@@ -437,8 +444,17 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       {
         float4 hc[4];
+        if (Hc) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hc[c] = f4_nt(Hc + ro + c * cs);
+          for (int c = 0; c < 4; ++c) hc[c] = f4_nt(Hc + ro + c * cs);
+        } else {  // layer 0: h0 = relu(W0 . x) of this lane's row (lin8, as the aggregation built it)
+          const float xk0 = rvalid ? a.x[((size_t)ep * N + n) * 8 + s4] : 0.f;
+          const float xk1 = rvalid ? a.x[((size_t)ep * N + n) * 8 + 4 + s4] : 0.f;
+          f32x4 z[4];
+          lin8(z, P + PK_W0, xk0, xk1, lane);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hc[c] = relu4(z[c]);
+        }
         mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
       }
       mm_bf3_seq(hn, mr, WL + 3 * BF_HALF, lane);
@@ -561,13 +577,15 @@ __global__ __launch_bounds__(256) void shared_readout_kernel(MpnnArgs a, SharedB
 static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStream_t st) {
   if (a.N > 2048) return fail(ECO_ERR_ARG, "shared-graph MPNN: N > 2048 does not fit one LDS block");
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
-  shared_perm_kernel<<<(a.N + 63) / 64, 64, 0, st>>>(a, sb);
+  shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.nt16 * 16 + 255) / 256, 256, 0, st>>>(a, sb);
-  shared_prep_kernel<<<(sb.ntiles * sb.S + SHP_WAVES - 1) / SHP_WAVES, 64 * SHP_WAVES, 0, st>>>(a, sb);
   const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks
   const int agrid = std::min(items, shared_grid());
   const size_t lds_agg = (size_t)a.N * 64;
-  (void)hipFuncSetAttribute((const void*)shared_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
+  (void)hipFuncSetAttribute((const void*)shared_agg_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
+  (void)hipFuncSetAttribute((const void*)shared_agg_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
+  (void)hipFuncSetAttribute((const void*)shared_agg_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
+  (void)hipFuncSetAttribute((const void*)shared_agg_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   const int grid = shared_grid();
   const size_t lds_edge = 24 * BF_FRAG * 2, lds_layer = 96 * BF_FRAG * 2;
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -576,16 +594,16 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
                             (int)lds_layer);
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_layer);
-  // the A- pass returns at once on graphs without -1 edges (meta[2], the smallest weight, read on the device)
-  shared_agg_kernel<<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.U, 1, 0, items);
-  shared_agg_kernel<<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.V, -1, 1, items);
+  // edge phase: A+ . U (+ A- . V; that pass returns at once on graphs without -1 edges, meta[2] on the device)
+  shared_agg_kernel<1><<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, nullptr, 1, 0, items);
+  shared_agg_kernel<2><<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, nullptr, -1, 1, items);
   shared_lin_kernel<0><<<grid, 64 * SH_NW, lds_edge, st>>>(a, sb, 0, nullptr, nullptr);
-  shared_agg_kernel<<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.HA, 0, 0, items);
-  shared_lin_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 0, sb.HA, sb.HB);
-  shared_agg_kernel<<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.HB, 0, 0, items);
-  shared_lin_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 1, sb.HB, sb.HA);
-  shared_agg_kernel<<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.HA, 0, 0, items);
-  shared_lin_kernel<2><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 2, sb.HA, nullptr);
+  shared_agg_kernel<3><<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, nullptr, 0, 0, items);       // A . h0
+  shared_lin_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 0, nullptr, sb.HB);           // h1
+  shared_agg_kernel<0><<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.HB, 0, 0, items);
+  shared_lin_kernel<1><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 1, sb.HB, sb.HA);             // h2
+  shared_agg_kernel<0><<<agrid, 64 * AG_NW, lds_agg, st>>>(a, sb, sb.HA, 0, 0, items);
+  shared_lin_kernel<2><<<grid, 64 * SH_NW, lds_layer, st>>>(a, sb, 2, sb.HA, nullptr);           // q_local, sums
   shared_readout_kernel<<<a.B, 256, 0, st>>>(a, sb);
   return check_launch("mpnn_forward_shared");
 }
