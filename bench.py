@@ -550,7 +550,7 @@ def inference_bench(args, world, rank, local, dev, dist):
             # row-wise Linears): HBM bytes of one forward from the committed PMC pass, over the live time
             tb = pmc_gset_traffic()
             out["roofline"]["traffic"] = tb
-            out["roofline"]["traffic_unit"] = "HBM bytes per forward (prep + aggregation + Linear launches; PMC, " + \
+            out["roofline"]["traffic_unit"] = "HBM bytes per forward (aggregation + Linear + table launches; PMC, " + \
                 os.path.relpath(PMC_GSET, REPO) + ")"
             if tb:
                 out["roofline"]["hbm"] = {"bound": "hbm", "achieved": tb / (fwd_ms * 1e-3) / 1e9, "unit": "GB/s",
