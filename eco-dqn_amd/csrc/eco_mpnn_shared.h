@@ -37,6 +37,11 @@ namespace eco {
 constexpr int SH_EPS = 4;              // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per Linear tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
 constexpr int SH_NW = SH_NW_X;         // waves per Linear workgroup (one workgroup per CU: <= 128 VGPRs at 16)
+#ifndef SH_PREFETCH
+#define SH_PREFETCH 0                  // 1: the next tile's rows are loaded while the current tile computes (measured
+                                       // slower: 3.96 ms per configs[4] step with 16 waves (49 VGPRs spill), 3.69
+                                       // with 8, against 3.56 without)
+#endif
 constexpr int SH_PART = SH_EPS * 64;   // floats of one tile's column-sum partial
 #ifndef AG_NW_X
 #define AG_NW_X 16
@@ -399,7 +404,46 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
   glds_wait();
   __syncthreads();
   const int total = sb.S * sb.ntiles;
-  for (int item = blockIdx.x * SH_NW + w; item < total; item += gridDim.x * SH_NW) {
+  // the rows of a tile: AG (all phases), e and h (update layers; layer 0 rebuilds h0 from x).  The NEXT
+  // item's rows are loaded while the current one's Linears run.
+  struct Rows {
+    float4 ag[4], ev[4], hc[4];
+    float xk0, xk1;
+  };
+  auto load_rows = [&](Rows& R, int it) {
+    const int s = it / sb.ntiles, t = it - s * sb.ntiles;
+    const int ep = s * SH_EPS + eps;
+    const int n = t * SH_NPT + kn;
+    const int nc = min(n, N - 1);
+    const size_t ro = sh_row(N, s, eps, nc, s4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) R.ag[c] = f4_nt(sb.AG + ro + c * cs);
+    if (PHASE != 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) R.ev[c] = f4_nt(sb.EB + ro + c * cs);
+      if (Hc) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) R.hc[c] = f4_nt(Hc + ro + c * cs);
+      } else {
+        const bool ok = ep < a.B && n < N;
+        R.xk0 = ok ? a.x[((size_t)ep * N + n) * 8 + s4] : 0.f;
+        R.xk1 = ok ? a.x[((size_t)ep * N + n) * 8 + 4 + s4] : 0.f;
+      }
+    }
+  };
+  int item = blockIdx.x * SH_NW + w;
+#if SH_PREFETCH
+  Rows nx;
+  if (item < total) load_rows(nx, item);
+#endif
+  for (; item < total; item += gridDim.x * SH_NW) {
+#if SH_PREFETCH
+    const Rows cu = nx;
+    if (item + gridDim.x * SH_NW < total) load_rows(nx, item + gridDim.x * SH_NW);
+#else
+    Rows cu;
+    load_rows(cu, item);
+#endif
     const int s = item / sb.ntiles, t = item - s * sb.ntiles;
     const int ep = s * SH_EPS + eps;
     const bool evalid = ep < a.B;
@@ -411,7 +455,7 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
     float4 acc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      acc[c] = f4_nt(sb.AG + ro + c * cs);
+      acc[c] = cu.ag[c];
       acc[c].x = acc[c].x / nf; acc[c].y = acc[c].y / nf; acc[c].z = acc[c].z / nf; acc[c].w = acc[c].w / nf;
     }
     const bool rvalid = nvalid && evalid;
@@ -430,32 +474,22 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       mm_bf3_seq(d, acc, WL, lane);               // message = relu(Wm . [agg, e])
-      {
-        float4 ev[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) ev[c] = f4_nt(sb.EB + ro + c * cs);
-        mm_bf3_seq(d, ev, WL + BF_HALF, lane);
-      }
+      mm_bf3_seq(d, cu.ev, WL + BF_HALF, lane);
       float4 mr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) mr[c] = relu4(d[c]);
       f32x4 hn[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      {
+      if (Hc) {
+        mm_bf3_seq(hn, cu.hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+      } else {  // layer 0: h0 = relu(W0 . x) of this lane's row (lin8, as the aggregation built it)
+        f32x4 z[4];
+        lin8(z, P + PK_W0, cu.xk0, cu.xk1, lane);
         float4 hc[4];
-        if (Hc) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) hc[c] = f4_nt(Hc + ro + c * cs);
-        } else {  // layer 0: h0 = relu(W0 . x) of this lane's row (lin8, as the aggregation built it)
-          const float xk0 = rvalid ? a.x[((size_t)ep * N + n) * 8 + s4] : 0.f;
-          const float xk1 = rvalid ? a.x[((size_t)ep * N + n) * 8 + 4 + s4] : 0.f;
-          f32x4 z[4];
-          lin8(z, P + PK_W0, xk0, xk1, lane);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) hc[c] = relu4(z[c]);
-        }
-        mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+        for (int c = 0; c < 4; ++c) hc[c] = relu4(z[c]);
+        mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);
       }
       mm_bf3_seq(hn, mr, WL + 3 * BF_HALF, lane);
       if (PHASE == 1) {
