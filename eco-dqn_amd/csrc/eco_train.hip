@@ -23,6 +23,9 @@ struct WJob {
   int out_col0;      // first column in the flat buffer
 };
 constexpr int MAX_JOBS = 10;
+#ifndef WGRAD_WG_X
+#define WGRAD_WG_X 3  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
+#endif
 constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
@@ -720,7 +723,7 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
     // gradient step of backward + weight gradients at M = 2048 ER-200)
     J.first[0] = 0;
     for (int j = 0; j < n; ++j) {
-      J.nwgj[j] = std::min(WG_PER_JOB, 3 * 256 / n);
+      J.nwgj[j] = std::min(WG_PER_JOB, WGRAD_WG_X * 256 / n);
       J.first[j + 1] = J.first[j] + J.nwgj[j];
     }
     wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
