@@ -329,10 +329,12 @@ def main():
     if args.dry_run:
         return dry_run_bench(args, world, rank, local)
     dist = world > 1
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on GPU 0, gloo collectives
+    gpu = 0 if os.environ.get("ECO_BENCH_SHARED_DEVICE") == "1" else local
     if dist:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        torch.distributed.init_process_group(os.environ.get("ECO_BENCH_BACKEND", "nccl"))
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     if args.workload in ("gset", "er20"):
