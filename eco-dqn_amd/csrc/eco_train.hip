@@ -317,7 +317,16 @@ __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad)
   if (o >= J.nO || i >= K) return;
   const float* s = slabs + (size_t)blockIdx.y * SLABS_PER_JOB * SLAB + o * 128 + i;
   float acc = 0.f;
-  for (int k = 0; k < jobs.nwgj[blockIdx.y]; ++k) acc += s[(size_t)k * SLAB];
+  const int nk = jobs.nwgj[blockIdx.y];
+  int k = 0;
+  for (; k + 8 <= nk; k += 8) {  // eight slab loads in flight, summed in slab order (same result as one by one)
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s[(size_t)(k + u) * SLAB];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < nk; ++k) acc += s[(size_t)k * SLAB];
   grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
 }
 
