@@ -212,6 +212,10 @@ size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch);
  * obs_x[B][N][ECO_OBS_X_STRIDE(n_obs_in)]: node features; adjacency = graphs graph_ids[B] of `gs`.
  * Up to 8 features every kernel applies; 9..16 features (MAIN_OBSERVABLES) run the CSR-gather kernels
  * for N <= 512 (the dense-aggregation and N > 512 kernels take 8-float rows).
+ * N > 512 with every graph id naming ONE graph of a single-graph set with +-1 weights (the GSet G22
+ * best-cut search of experiments/test_eco.py) takes the shared-graph kernels: the aggregation A.[H_1..H_B]
+ * from LDS-staged per-episode blocks, N <= 2048; the workspace (eco_mpnn_workspace_bytes) holds their
+ * node-major buffers.
  * q[B][N] fp32 (may be NULL when only actions are wanted).
  * act / actions[B]: optional fused epsilon-greedy action selection.
  * saved: NULL for inference; for the training forward of train_step (dqn.py:437)
