@@ -949,11 +949,21 @@ __global__ __launch_bounds__(64 * NW, 2) void mpnn_forward_large_kernel(MpnnArgs
   readout_act<false, NW>(a, Hc, 64, Scr, true, e, 1, N, R0, RT);
 }
 
-__global__ void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, int B, int* out) {
+// norm.max() of the call (mpnn.py:102 over every graph of the batch): ONE workgroup reduces all B graph
+// ids and writes the result (no zeroing memset, no atomics)
+__global__ __launch_bounds__(1024) void call_maxdeg_kernel(const eco_graph_set gs, const int32_t* gids, int B,
+                                                           int* out) {
+  __shared__ int red[16];
   int m = 1;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) m = max(m, gs.max_deg[gids[i]]);
+  for (int i = threadIdx.x; i < B; i += blockDim.x) m = max(m, gs.max_deg[gids[i]]);
   m = wave_max_i(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int r = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = max(r, red[w]);
+    *out = r;
+  }
 }
 
 static int prepare(MpnnArgs& a, const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
@@ -1091,8 +1101,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   if (act) a.act = *act;
   a.actions = actions;
   if (norm_scope == ECO_NORM_PER_CALL) {
-    if (hipMemsetAsync(cmax, 0, sizeof(int), st) != hipSuccess) return fail(ECO_ERR_HIP, "memset failed");
-    call_maxdeg_kernel<<<min(256, (batch + 255) / 256), 256, 0, st>>>(*gs, graph_ids, batch, cmax);
+    call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE"))
     return mpnn_forward_dense_launch(a, saved != nullptr, st);
