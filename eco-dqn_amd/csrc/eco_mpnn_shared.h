@@ -58,6 +58,7 @@ constexpr int AG_TPW = AG_TPW_X;       // aggregation tiles per wave in flight t
 #define AG_DEPTH2 0                    // 1: edge words loaded two groups ahead instead of one
 #endif
 constexpr int AG_UNROLL = AG_UNROLL_X; // edge words in flight per lane
+static_assert(AG_UNROLL % 4 == 0, "edge words are loaded in 16-B groups");
 
 struct SharedBufs {
   float* HA;      // [S][4][SH_EPS][N][16]: h2 (h0, U and V are never stored: the aggregation launches and the
@@ -69,7 +70,8 @@ struct SharedBufs {
   int32_t* perm;  // [N] nodes by decreasing degree
   int32_t* tn;    // [nt16][16] aggregation tiles: node of each slot (-1: none), 16 ranked nodes per tile
   int32_t* tml;   // [nt16] the tile's longest CSR row, rounded up to AG_UNROLL
-  uint32_t* et;   // [nt16][MD][16] the tile's CSR rows interleaved (edge i of slot k at i * 16 + k; padding: 0)
+  uint32_t* et;   // [nt16][MD / 4][16][4] the tile's CSR rows interleaved, four consecutive edges of a slot in one
+                  // 16-B word group (edge i of slot k at ((i >> 2) * 16 + k) * 4 + (i & 3); padding: 0)
   int Epad, S, ntiles, nt16, MD;
 };
 
@@ -87,8 +89,8 @@ inline int shared_grid() {  // persistent Linear workgroups: one per CU
 inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
   const size_t nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
-  const size_t nt16 = ((size_t)N + 15) / 16, MD = (size_t)N + AG_UNROLL;
-  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + nt16 * MD * 16) *
+  const size_t nt16 = ((size_t)N + 15) / 16, MD = ((size_t)N + 3) / 4 * 4 + AG_UNROLL;
+  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + 4 + nt16 * MD * 16) *
          sizeof(float);
 }
 
@@ -106,10 +108,10 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.ql = sb.part + (size_t)sb.S * sb.ntiles * SH_PART;
   sb.perm = reinterpret_cast<int32_t*>(sb.ql + (size_t)sb.Epad * N);
   sb.nt16 = (N + 15) / 16;
-  sb.MD = N + AG_UNROLL;
+  sb.MD = (N + 3) / 4 * 4 + AG_UNROLL;
   sb.tn = sb.perm + N;
   sb.tml = sb.tn + (size_t)sb.nt16 * 16;
-  sb.et = reinterpret_cast<uint32_t*>(sb.tml + sb.nt16);
+  sb.et = reinterpret_cast<uint32_t*>(((uintptr_t)(sb.tml + sb.nt16) + 15) & ~(uintptr_t)15);  // 16-B groups
   return sb;
 }
 
@@ -212,8 +214,8 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
   const int ml = (rp[n0 + 1] - rp[n0] + AG_UNROLL - 1) / AG_UNROLL * AG_UNROLL;
   sb.tn[slot] = valid ? n : -1;
   if (k == 0) sb.tml[t] = ml;
-  uint32_t* et = sb.et + (size_t)t * sb.MD * 16 + k;
-  for (int q = 0; q < max(ml, AG_UNROLL); ++q) et[q * 16] = q < len ? eg[rp[n] + q] : 0u;
+  uint32_t* et = sb.et + (size_t)t * sb.MD * 16;
+  for (int q = 0; q < max(ml, AG_UNROLL); ++q) et[((q >> 2) * 16 + k) * 4 + (q & 3)] = q < len ? eg[rp[n] + q] : 0u;
 }
 
 // AG[item] (+)= A^(mode) . src[item] for the items = (slice, chunk, episode) blocks: an item's [N][16] block
@@ -295,6 +297,14 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = lane >> 2, q = lane & 3;
+  // edges i .. i + AG_UNROLL - 1 of a slot: AG_UNROLL / 4 16-B loads (i a multiple of 4)
+  auto load_group = [](const uint32_t* e, int i, uint32_t(&dst)[AG_UNROLL]) {
+#pragma unroll
+    for (int g = 0; g < AG_UNROLL / 4; ++g) {
+      const uint4 v = *reinterpret_cast<const uint4*>(e + ((i >> 2) + g) * 64);
+      dst[4 * g] = v.x; dst[4 * g + 1] = v.y; dst[4 * g + 2] = v.z; dst[4 * g + 3] = v.w;
+    }
+  };
   for (; item < items; item += gridDim.x) {
     const bool more = item + (int)gridDim.x < items;
     if (more) load_block(item + gridDim.x);  // lands while this item is aggregated
@@ -312,16 +322,14 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
       for (int j = 0; j < AG_TPW; ++j) {
         const int t = tb + j * AG_NW;
         const bool live = t < sb.nt16;  // wave-uniform
-        et[j] = sb.et + (size_t)(live ? t : tb) * sb.MD * 16 + k;
-#pragma unroll
-        for (int u = 0; u < AG_UNROLL; ++u) cur[j][u] = et[j][u * 16];
+        et[j] = sb.et + (size_t)(live ? t : tb) * sb.MD * 16 + 4 * k;  // slot k's groups, 64 words apart
+        load_group(et[j], 0, cur[j]);
         nd[j] = live ? sb.tn[t * 16 + k] : -1;
         ml[j] = live ? uniform_i(sb.tml[t]) : 0;
         acc[j] = zero4();
 #if AG_DEPTH2
         if (AG_UNROLL < ml[j]) {
-#pragma unroll
-          for (int u = 0; u < AG_UNROLL; ++u) nxt[j][u] = et[j][(AG_UNROLL + u) * 16];
+          load_group(et[j], AG_UNROLL, nxt[j]);
         }
 #endif
       }
@@ -330,13 +338,11 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
         for (int j = 0; j < AG_TPW; ++j) {
 #if AG_DEPTH2
           if (i + 2 * AG_UNROLL < ml[j]) {
-#pragma unroll
-            for (int u = 0; u < AG_UNROLL; ++u) nx2[j][u] = et[j][(i + 2 * AG_UNROLL + u) * 16];  // two groups ahead
+            load_group(et[j], i + 2 * AG_UNROLL, nx2[j]);  // two groups ahead
           }
 #else
           if (i + AG_UNROLL < ml[j]) {
-#pragma unroll
-            for (int u = 0; u < AG_UNROLL; ++u) nxt[j][u] = et[j][(i + AG_UNROLL + u) * 16];  // next group in flight
+            load_group(et[j], i + AG_UNROLL, nxt[j]);  // next group in flight
           }
 #endif
         }
