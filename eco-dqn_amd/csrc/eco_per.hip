@@ -36,6 +36,20 @@ struct eco_per {
 
 namespace {
 
+// torch's float32 `tensor.pow(python_float)` (utils.py:266): the exponent rounded to float32; 0.5, 2, 3,
+// -0.5, -1, -2 are sqrt / square / cube / 1/sqrt / reciprocal / 1/square in float32, any other exponent a
+// float32 pow (correctly rounded here; torch's vectorised powf agrees to 1 ulp).
+float torch_pow_f32(float x, double exponent) {
+  const float e = (float)exponent;
+  if (e == 0.5f) return std::sqrt(x);
+  if (e == 2.0f) return x * x;
+  if (e == 3.0f) return x * x * x;
+  if (e == -0.5f) return 1.0f / std::sqrt(x);
+  if (e == -1.0f) return 1.0f / x;
+  if (e == -2.0f) return 1.0f / (x * x);
+  return (float)std::pow((double)x, (double)e);
+}
+
 void put(eco_per* p, int32_t h, int32_t b, double t) {  // __update_heap (utils.py:144-149)
   if (h > p->size) p->size = h;
   p->bp[h] = b;
@@ -234,8 +248,7 @@ extern "C" int eco_per_sample_finish(eco_per* p, int32_t batch, const int64_t* r
     const int64_t r = ranks ? ranks[k] : lo + (int64_t)(next_u64(s) % (uint64_t)(hi - lo));
     if (ranks_out) ranks_out[k] = r;
     buffer_positions[k] = p->bp[r];
-    // torch.FloatTensor probabilities, float32 N * p, pow with the double exponent rounded to float32
-    const float w = (float)std::pow((double)(nf * (float)p->probs[r - 1]), -p->beta);
+    const float w = torch_pow_f32(nf * (float)p->probs[r - 1], -p->beta);
     weights[k] = w;
     wmax = std::max(wmax, w);
   }

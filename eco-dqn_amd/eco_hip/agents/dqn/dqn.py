@@ -29,6 +29,15 @@ from ...parallel import allreduce_gradients, broadcast_parameters
 from .utils import CompactReplayBuffer, ReplayBuffer, TestMetric, set_global_seed
 
 
+def graph_slots_needed(n_envs, max_steps, replay_buffer_size):
+    """GraphStore slots for fresh graphs per episode with lockstep episodes (each ends at max_steps):
+    a batch of n_envs episodes pushes n_envs * max_steps transitions, and a batch's slots may only be
+    regenerated once replay_buffer_size pushes have passed since it ended, so
+    ceil(replay_buffer_size / (n_envs * max_steps)) + 1 batches of n_envs slots rotate."""
+    per_batch = n_envs * max_steps
+    return n_envs * (-(-int(replay_buffer_size) // per_batch) + 1)
+
+
 class DQN:
     def __init__(self, envs, network, init_network_params=None, init_weight_std=None, double_dqn=True,
                  update_target_frequency=10000, gamma=0.99, clip_Q_targets=False, replay_start_size=50000,
@@ -67,7 +76,9 @@ class DQN:
         self.final_learning_rate_step = final_learning_rate_step
         self.weight_decay = weight_decay
         self.update_frequency = update_frequency
-        self.update_exploration = update_exploration
+        # dqn.py:161 stores a one-tuple (`self.update_exploration = update_exploration,`), which is always
+        # truthy: the reference decays epsilon whatever is passed, and so does this class
+        self.update_exploration = update_exploration,
         self.initial_exploration_rate = initial_exploration_rate
         self.epsilon = initial_exploration_rate
         self.final_exploration_rate = final_exploration_rate
@@ -120,15 +131,32 @@ class DQN:
         self._samples_since_sync = 0.0
         self.graph_pool_ids = (np.arange(self.graphs.n_graphs) if graph_pool_ids is None
                                else np.asarray(graph_pool_ids))
-        # Fresh graphs per episode like the reference's generators (utils.py:165-236): the store
-        # holds 2B slots, episode batch k runs on half k % 2 while the other half is regenerated on
-        # the device.  Replay entries reference graph ids, so a half is only regenerated once every
-        # entry pushed while it was in use has been overwritten (_switch_graph_half).
+        # Fresh graphs per episode like the reference's generators (utils.py:165-236): every reset
+        # takes the next slots of the store in ring order and regenerates them on the device first.
+        # Replay entries reference graph ids, so a slot is only regenerated once no live episode uses
+        # it and `replay_buffer_size` pushes have passed since its last episode ended (every entry
+        # that could reference it has been overwritten); otherwise its graph is reused as it is
+        # (still correct, not fresh) and a warning is issued once.
         self.regenerate_graphs = regenerate_graphs
-        self._pool_half = 0
+        self._pushed = 0
         if regenerate_graphs is not None:
-            if self.graphs.n_graphs < 2 * envs.n_envs or not hasattr(self.graphs, "cap"):
-                raise ValueError("regenerate_graphs needs GraphStore.slots(2 * n_envs, ...)")
+            if not hasattr(self.graphs, "cap"):
+                raise ValueError("regenerate_graphs needs a GraphStore.slots(...) store")
+            need = graph_slots_needed(envs.n_envs, envs.max_steps, replay_buffer_size)
+            if envs.reversible_spins and envs.cfg.stopping == 1 and self.graphs.n_graphs < need:
+                # lockstep episodes (every one ends at max_steps): B * max_steps pushes per episode batch,
+                # so ceil(capacity / (B * max_steps)) + 1 batches of B slots must rotate
+                raise ValueError(f"regenerate_graphs with n_envs={envs.n_envs}, max_steps={envs.max_steps} and "
+                                 f"replay_buffer_size={replay_buffer_size} needs GraphStore.slots(>= {need}, ...) "
+                                 f"(has {self.graphs.n_graphs}): a slot may only be regenerated once no stored "
+                                 "transition references it")
+            n_slots = self.graphs.n_graphs
+            self._slot_users = np.zeros(n_slots, np.int64)
+            self._slot_free_at = np.full(n_slots, -(1 << 62), np.int64)
+            self._slot_cursor = 0
+            self._slot_warned = False
+            self.graphs_regenerated = 0      # slots regenerated so far (fresh graphs handed out)
+            self.graphs_reused = 0           # slots handed out without regeneration (not yet safe)
         self._rng = np.random.default_rng(self.seed)
 
         self.evaluate = evaluate
@@ -204,10 +232,12 @@ class DQN:
         return out
 
     # ----------------------------------------------------------------- train
-    def train_step(self, transitions, sync_loss=True):
+    def train_step(self, transitions, sync_loss=True, loss_out=None):
         """dqn.py:403-451.  transitions = (states_x, actions, rewards, states_next_x, dones, graph_ids)
-        as returned by ReplayBuffer.sample.  Returns the loss (float if sync_loss else device tensor)."""
+        as returned by ReplayBuffer.sample.  Returns the loss: a float if sync_loss, else the one-element
+        device tensor it was written to (`loss_out`, or a copy of the agent's loss slot)."""
         xs, act, rew, xn, done, gid = transitions
+        loss_dev = self.loss_dev if loss_out is None else loss_out
         m = xs.shape[0]
         if m != self._train_m:
             self._alloc_train_buffers(m)
@@ -226,7 +256,7 @@ class DQN:
         _lib.check(_lib.lib.eco_dqn_td(_lib.ptr(self.q_s), _lib.ptr(self.q_tn), _lib.ptr(self.a_star),
                                        _lib.ptr(act), _lib.ptr(rew), _lib.ptr(done), m, self.N,
                                        ctypes.c_float(self.gamma), int(bool(self.clip_Q_targets)), _lib.ptr(self.dq),
-                                       _lib.ptr(self.sqerr), _lib.ptr(self.loss_dev), _lib.stream_ptr()))
+                                       _lib.ptr(self.sqerr), _lib.ptr(loss_dev), _lib.stream_ptr()))
         net.backward_graphs(xs, self.graphs, gid, self.saved, self.dq, self.grad, workspace=self.bw_ws)
         scale = allreduce_gradients(self.grad)  # RCCL sum over xGMI (233.7 KB), mean folded into Adam
         self.adam_step += 1
@@ -237,35 +267,51 @@ class DQN:
         net.repack()
         self.grad_steps += 1
         self._samples_since_sync += m * self.world
-        return self.loss_dev.item() if sync_loss else self.loss_dev.clone()
+        if sync_loss:
+            return loss_dev.item()
+        return loss_dev if loss_out is not None else loss_dev.clone()
 
     def sync_target(self):
         """dqn.py:346-347: target <- online."""
         self.target_network.flat.copy_(self.network.flat)
 
-    def _switch_graph_half(self, n):
-        """Graph ids for a full reset.  With regenerate_graphs the store holds two halves of B
-        slots: the next batch runs on the other half, regenerated on the device first -- unless a
-        replay entry may still reference it (fewer than `capacity` pushes since that half was last
-        in use, e.g. episodes shorter than max_steps), in which case its graphs are reused."""
-        if self.regenerate_graphs is not None:
-            kind, param = self.regenerate_graphs[:2]
-            weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
-            self._half_last_push[self._pool_half] = self._pushed
-            half = self._pool_half ^ 1
-            self._pool_half = half
-            if self._pushed - self._half_last_push[half] >= self.replay_buffer_size:
-                self.graphs.generate(half * self.B, self.B, kind, param,
-                                     seed=int(self._rng.integers(1 << 62)), weights=weights)
-            return half * self.B + np.arange(n)
-        return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
-
-    def _random_graph_ids(self, n):
-        """Graph ids for episodes reset on their own (an episode that ended before the others):
-        random graphs of the active half (regenerate_graphs) or of the pool."""
-        if self.regenerate_graphs is not None:
-            return self._pool_half * self.B + self._rng.integers(0, self.B, n)
-        return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), n)]
+    def _take_graph_slots(self, episodes):
+        """Graph ids for the episodes being reset (a bool mask over B, or None = all).  Without
+        regenerate_graphs: random graphs of the pool.  With it: the next slots of the store in ring
+        order, each regenerated on the device when it is safe (no live user, `replay_buffer_size`
+        pushes since its last episode ended), reused otherwise (warned once)."""
+        k = self.B if episodes is None else int(episodes.sum())
+        if self.regenerate_graphs is None:
+            return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), k)]
+        kind, param = self.regenerate_graphs[:2]
+        weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
+        n_slots = len(self._slot_users)
+        if self._started:   # release the slots of the episodes being reset
+            old = self.env.graph_ids.cpu().numpy()
+            old = old if episodes is None else old[episodes]
+            np.subtract.at(self._slot_users, old, 1)
+            self._slot_free_at[old[self._slot_users[old] == 0]] = self._pushed
+        ids = (self._slot_cursor + np.arange(k)) % n_slots
+        self._slot_cursor = int((self._slot_cursor + k) % n_slots)
+        safe = (self._slot_users[ids] == 0) & (self._pushed - self._slot_free_at[ids] >= self.replay_buffer_size)
+        fresh = ids[safe]
+        for run in np.split(fresh, np.nonzero(np.diff(fresh) != 1)[0] + 1) if len(fresh) else []:
+            self.graphs.generate(int(run[0]), len(run), kind, param, seed=int(self._rng.integers(1 << 62)),
+                                 weights=weights, check=False)
+        self.graphs_regenerated += len(fresh)
+        self.graphs_reused += k - len(fresh)
+        if len(fresh) < k and not self._slot_warned:
+            import warnings
+            warnings.warn(f"regenerate_graphs: {k - len(fresh)} of {k} episodes reset onto graphs that stored "
+                          f"transitions may still reference (store of {n_slots} slots); they reuse those graphs. "
+                          "Allocate more GraphStore.slots for a fresh graph per episode.", RuntimeWarning)
+            self._slot_warned = True
+        np.add.at(self._slot_users, ids, 1)
+        if episodes is None:
+            return ids
+        out = np.zeros(self.B, np.int64)
+        out[episodes] = ids
+        return out
 
     def vector_step(self, is_training_ready):
         """One act -> env.step -> replay.add over all B episodes; returns the new obs buffer.
@@ -289,16 +335,21 @@ class DQN:
             self.replay_buffer.snapshot(mask)
 
     def start(self):
-        """Reset every episode on fresh pool graphs (start of learn)."""
-        self._pushed = 0
-        self._half_last_push = [-(1 << 62), -(1 << 62)]
-        self._reset_env(self._switch_graph_half(self.B), self.seed)
+        """Reset every episode on fresh pool graphs (start of learn).  The replay buffer and the push
+        count persist across learn() calls (as the reference's replay buffer does), so graph slots that
+        stored transitions reference are not regenerated by a second learn()."""
+        self._started = getattr(self, "_started", False)
+        self._reset_env(self._take_graph_slots(None), self.seed)
+        self._started = True
         self._steps_in_episode = 0
         self._timestep = 0
         self._ready = False
         self._k_per_vec = max(1, int(round(self.B * self.replay_ratio / self.M)))
         self._last_loss = None
-        self._loss_log = []
+        if not hasattr(self, "_loss_buf"):   # every gradient step's loss, kept on the device (dqn.py:339)
+            self._loss_buf = torch.zeros(4096, dtype=torch.float32, device=self.device)
+            self._loss_t = np.zeros(4096, np.int64)
+            self._loss_n = 0
         # every episode ends exactly at max_steps only for reversible spins with Stopping.NORMAL
         # (spinsystem.py:539-554); otherwise dones are read back after each vector step
         self._lockstep = self.env.reversible_spins and self.env.cfg.stopping == 1
@@ -313,32 +364,43 @@ class DQN:
         self.vector_step(self._ready)
         self._timestep += B * self.world
         self._steps_in_episode += 1
+        # dqn.py:284-290 run after each act with that env-step's 0-based index: a vector step ends with
+        # the index of its last env-step (B = 1 reproduces the reference's sequence exactly)
         if self.update_exploration:
-            self.update_epsilon(self._timestep)
+            self.update_epsilon(self._timestep - 1)
         if self.update_learning_rate:
-            self.update_lr(self._timestep)
+            self.update_lr(self._timestep - 1)
         if self._lockstep:
             if self._steps_in_episode == T:
-                self._reset_env(self._switch_graph_half(B), self.seed + self._timestep)
+                self._reset_env(self._take_graph_slots(None), self.seed + self._timestep)
                 self._steps_in_episode = 0
         else:
             done = self.env.dones.bool()
             n_done = int(done.sum())
             if n_done == B:
-                self._reset_env(self._switch_graph_half(B), self.seed + self._timestep)
+                self._reset_env(self._take_graph_slots(None), self.seed + self._timestep)
                 self._steps_in_episode = 0
             elif n_done:
-                self._reset_env(self._random_graph_ids(B), self.seed + self._timestep, mask=done)
+                mask = done.cpu().numpy()
+                self._reset_env(self._take_graph_slots(mask), self.seed + self._timestep, mask=done)
         if self._ready:
-            step_losses = []
             for _ in range(self._k_per_vec):
-                self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False)
-                step_losses.append(self._last_loss)
+                self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False,
+                                                  loss_out=self._loss_slot(self._timestep))
                 if self._samples_since_sync >= self.target_sync_samples:
                     self.sync_target()
                     self._samples_since_sync = 0.0
-            self._loss_log.append((self._timestep, torch.cat(step_losses)))
         return self._last_loss
+
+    def _loss_slot(self, timestep):
+        """One-element view of the device loss log for the next gradient step (grown by doubling, so
+        the log costs no allocation per step and one host copy in losses())."""
+        if self._loss_n == len(self._loss_t):
+            self._loss_buf = torch.cat([self._loss_buf, torch.zeros_like(self._loss_buf)])
+            self._loss_t = np.concatenate([self._loss_t, np.zeros_like(self._loss_t)])
+        self._loss_t[self._loss_n] = timestep
+        self._loss_n += 1
+        return self._loss_buf[self._loss_n - 1:self._loss_n]
 
     def learn(self, timesteps, verbose=False, on_vector_step=None):
         """dqn.py:256-395 with B episodes per vector step on each rank (timesteps counts global
@@ -392,11 +454,11 @@ class DQN:
 
     def losses(self):
         """[[timestep, loss], ...] of every gradient step so far (dqn.py:339, one host copy)."""
-        out = []
-        for t, l in self._loss_log:
-            for v in l.cpu().tolist():
-                out.append([t, v])
-        return out
+        n = getattr(self, "_loss_n", 0)
+        if n == 0:
+            return []
+        vals = self._loss_buf[:n].cpu().tolist()
+        return [[int(t), v] for t, v in zip(self._loss_t[:n], vals)]
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()

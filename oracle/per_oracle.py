@@ -15,6 +15,21 @@ import math
 import numpy as np
 
 
+def torch_pow_f32(x, exponent):
+    """torch's float32 `tensor.pow(python_float)`: the exponent is rounded to float32; the exponents
+    0.5, 2, 3, -0.5, -1, -2 take sqrt / square / cube / 1/sqrt / reciprocal / 1/square in float32;
+    any other is pow with a float32 result (computed here correctly rounded from float64; torch's
+    vectorised powf agrees to 1 ulp)."""
+    x = np.asarray(x, np.float32)
+    e = np.float32(exponent)
+    one = np.float32(1)
+    special = {0.5: lambda v: np.sqrt(v), 2.0: lambda v: v * v, 3.0: lambda v: v * v * v,
+               -0.5: lambda v: one / np.sqrt(v), -1.0: lambda v: one / v, -2.0: lambda v: one / (v * v)}
+    if float(e) in special:
+        return special[float(e)](x).astype(np.float32)
+    return np.power(x.astype(np.float64), np.float64(e)).astype(np.float32)
+
+
 class PEROracle:
     def __init__(self, capacity=10000, alpha=0.7, beta0=0.5):  # utils.py:88-111
         self.capacity = capacity
@@ -131,8 +146,7 @@ class PEROracle:
         bps = [self.bp[r] for r in ranks]
         n = self.capacity if self.full else self.size
         p = np.array([self.probabilities[r] for r in ranks], dtype=np.float32)
-        # torch: float32 N * p, raised to the (double) -beta and rounded back to float32
-        w = ((np.float32(n) * p).astype(np.float64) ** (-self.beta)).astype(np.float32)
+        w = torch_pow_f32(np.float32(n) * p, -self.beta)    # utils.py:266 (N * FloatTensor).pow(-beta)
         w = w / w.max()
         return list(ranks), bps, w
 

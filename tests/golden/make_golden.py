@@ -371,6 +371,35 @@ def make_schedules():
     np.savez_compressed(os.path.join(HERE, "schedules.npz"), **out)
 
 
+def make_exploration():
+    """DQN.learn's epsilon trace (dqn.py:284-286) with update_exploration False and True: dqn.py:161 stores
+    a one-tuple, so epsilon decays either way.  update_epsilon is wrapped to record (timestep, epsilon)
+    after every call; replay_start_size > timesteps, so no train_step runs."""
+    n, T = 20, 60
+    J = graphs.er_graph(n, 0.15, np.random.default_rng(8))
+    net_fn = lambda: MPNN(n_obs_in=7, n_layers=3, n_features=64, n_hid_readout=[], tied_weights=False)  # noqa: E731
+    out = {}
+    for flag in (False, True):
+        env = ising_env.make("SpinSystem", SingleGraphGenerator(J), 2 * n, **env_args("eco", n))
+        agent = DQN([env], net_fn, replay_start_size=10 ** 6, replay_buffer_size=1000, logging=False,
+                    evaluate=False, seed=1, network_save_path="/tmp/n.pth", test_save_path="/tmp/ts.pkl",
+                    update_exploration=flag, initial_exploration_rate=1, final_exploration_rate=0.1,
+                    final_exploration_step=40, update_learning_rate=False, initial_learning_rate=1e-4)
+        trace = []
+        orig = agent.update_epsilon
+
+        def rec(t, orig=orig, trace=trace):
+            orig(t)
+            trace.append((t, agent.epsilon))
+        agent.update_epsilon = rec
+        agent.learn(T)
+        out[f"{int(flag)}/attr_truthy"] = np.bool_(bool(agent.update_exploration))
+        out[f"{int(flag)}/timesteps"] = np.array([t for t, _ in trace], dtype=np.int64)
+        out[f"{int(flag)}/eps"] = np.array([e for _, e in trace], dtype=np.float64)
+        out[f"{int(flag)}/final_eps"] = np.float64(agent.epsilon)
+    np.savez_compressed(os.path.join(HERE, "exploration.npz"), **out)
+
+
 def make_greedy_rollout():
     """Pretrained-net greedy rollout (dqn.py:490-512 predict) on one ER-200 graph:
     actions plus the top-1/top-2 Q margin per step (argmax-tie robustness)."""
@@ -535,7 +564,7 @@ def make_env_problems():
 if __name__ == "__main__":
     random.seed(0)
     np.random.seed(0)
-    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "dqn_step_s2v", "schedules",
+    which = sys.argv[1:] or ["env_er20", "env_large", "mpnn", "dqn_step", "dqn_step_s2v", "schedules", "exploration",
                               "greedy_rollout", "greedy_solver",
                               "env_problems"]
     for w in which:

@@ -398,3 +398,60 @@ def test_compact_replay_matches_feature_replay(n, B, basis):
         for u, v in zip(a, b):
             assert torch.equal(u.view(torch.int32) if u.dtype == torch.float32 else u,
                                v.view(torch.int32) if v.dtype == torch.float32 else v)
+
+
+@pytest.mark.parametrize("flag", [False, True])
+def test_update_exploration_quirk_matches_reference(flag):
+    """dqn.py:161 stores `update_exploration` as a one-tuple, so learn() decays epsilon even when False is
+    passed (:285-286).  tests/golden/exploration.npz records the reference's epsilon after every
+    update_epsilon call of a 60-step learn(); one episode (B = 1) reproduces that sequence exactly."""
+    from eco_hip.graphs import GraphStore
+    f = np.load(os.path.join(GOLDEN, "exploration.npz"))
+    key = str(int(flag))
+    assert bool(f[key + "/attr_truthy"])
+    n = 20
+    store = GraphStore.random("ER", 4, n, 0.15, seed=8)
+    agent = _dqn_for(store, n, B=1, update_exploration=flag, initial_exploration_rate=1, final_exploration_rate=0.1,
+                     final_exploration_step=40, replay_start_size=10 ** 6, replay_buffer_size=1000)
+    assert bool(agent.update_exploration)
+    trace = []
+    agent.learn(timesteps=len(f[key + "/eps"]), on_vector_step=lambda t: trace.append(agent.epsilon))
+    np.testing.assert_array_equal(np.array(trace), f[key + "/eps"])
+    assert agent.epsilon == float(f[key + "/final_eps"])
+
+
+def test_regenerate_graphs_with_replay_longer_than_an_episode_batch():
+    """replay capacity > B * max_steps.  Lockstep episodes need ceil(C / (B T)) + 1 batches of B
+    graph slots in rotation (a smaller store is rejected); with them every episode batch runs on graphs
+    regenerated on the device, and no slot is regenerated while a stored transition may reference it."""
+    from eco_hip.graphs import GraphStore, edge_cap
+    from eco_hip.agents.dqn.dqn import graph_slots_needed
+    n, B = 20, 64
+    T = 2 * n
+    C = B * T * 2 + 100                       # 2.04 episode batches of transitions
+    need = graph_slots_needed(B, T, C)
+    assert need == 4 * B
+    with pytest.raises(ValueError, match="GraphStore.slots"):
+        _dqn_for(GraphStore.slots(2 * B, n, edge_cap("ER", n, 0.15)), n, B=B, replay_buffer_size=C,
+                 regenerate_graphs=("ER", 0.15))
+    st = GraphStore.slots(need, n, edge_cap("ER", n, 0.15))
+    agent = _dqn_for(st, n, B=B, replay_buffer_size=C, replay_start_size=B * 4, train_minibatch=128,
+                     regenerate_graphs=("ER", 0.15))
+    seen = []
+
+    def snap(t):
+        if agent._steps_in_episode == 0:       # a full reset just happened
+            seen.append((agent.env.graph_ids.cpu().numpy().copy(), st.edges.clone(), agent._pushed))
+    agent.learn(timesteps=B * T * 6, on_vector_step=snap)
+    agent.env.check_errors()
+    assert agent.graphs_reused == 0 and agent.graphs_regenerated == B * 7
+    assert len(seen) == 6
+    for i in range(1, len(seen)):
+        ids_prev, ids = seen[i - 1][0], seen[i][0]
+        assert not set(ids_prev) & set(ids)                       # a new batch of slots each time
+        # the slots handed out were regenerated: their edges differ from what they held before
+        assert not torch.equal(seen[i][1], seen[i - 1][1])
+    # slot batch k is reused at batch k + 4: by then >= C pushes have passed since it was left
+    assert np.array_equal(np.sort(seen[4][0]), np.sort(seen[0][0]))
+    assert seen[4][2] - seen[1][2] >= C
+    assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()

@@ -2,7 +2,9 @@
 libecohip.so (eco_per_*, host-only calls, no GPU needed) replayed through the scripted call sequences the
 reference itself was run through (tests/golden/make_per_golden.py -> per.npz).  Bars: heap layout (buffer
 position and td error per heap position), partitions, ranks -> buffer positions and beta exact; float32
-importance weights within 2 ulp (torch's float pow vs powf)."""
+importance weights bitwise for torch's special-cased exponents (beta = 0.5: 1/sqrt) and within 2 ulp
+otherwise (torch's vectorised powf is 1-ulp accurate, the restatements round correctly, and the
+normalisation by the batch maximum can add one more)."""
 import ctypes
 import os
 import sys
@@ -46,6 +48,13 @@ def close_f32(a, b):
     return np.all(np.abs(a.view(np.int32).astype(np.int64) - b.view(np.int32).astype(np.int64)) <= 2)
 
 
+def weights_ok(w, ref, beta):
+    """bitwise where torch special-cases the exponent (-0.5 -> 1/sqrt, -1 -> reciprocal), else 2 ulp"""
+    if np.float32(-beta) in (np.float32(-0.5), np.float32(-1.0)):
+        return np.array_equal(np.asarray(w, np.float32).view(np.int32), np.asarray(ref, np.float32).view(np.int32))
+    return close_f32(w, ref)
+
+
 @pytest.mark.parametrize("ci", [0, 1, 2])
 def test_oracle_matches_reference(ci):
     cap, alpha, beta0, anneal = case_params(ci)
@@ -65,7 +74,7 @@ def test_oracle_matches_reference(ci):
             assert [tuple(p) for p in o.partitions] == [tuple(p) for p in parts]
             assert bps == sbp.tolist()
             assert [newest[b] for b in bps] == sids.tolist()   # ring slot = buffer position - 1, newest add
-            assert close_f32(w, sw)
+            assert weights_ok(w, sw, beta), (beta, w, sw)
             n_samples += 1
         else:
             o.rebalance()
@@ -123,7 +132,7 @@ def test_native_heap_matches_reference(ci):
                    rout.ctypes.data_as(ctypes.c_void_p))
             np.testing.assert_array_equal(bps, sbp)
             np.testing.assert_array_equal(rout, ranks)
-            assert close_f32(w, sw), (w, sw)
+            assert weights_ok(w, sw, beta), (beta, w, sw)
             # the sampled transitions named their buffer position when added (ids = add counter); the ring
             # slot of a buffer position holds the newest add there
             assert len(sids) == n
