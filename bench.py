@@ -94,20 +94,23 @@ def _cpu_model():
         return platform.processor() or platform.machine()
 
 
-def cpu_refcost_baseline(n=200, seconds=10.0):
+def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
     """SURVEY.md 8d CPU side-by-side: the reference-cost restatement of env.step (oracle/refcost.py:
     the reference's per-step op mix -- 4 dense J@s matvecs, 2 dense np.outer cuts, the observables
     loop, the list-of-sets visited buffer and the vstack observation; bit-exact with the reference
     and calibrated against it in the build container, oracle/refcost_calibration.json) with a
     uniform random policy (configs[0]'s plumbing loop) on fresh ER(n, 0.15) graphs, one single-
-    threaded process per host core of this job's CPU share (at most 16 per GPU on the box), all at
-    once.  value = the sum of the per-process rates; only env.step is timed."""
+    threaded process per CPU of this process's affinity set (every host core it may use), all at
+    once.  value = the sum of the per-process rates (each timed over its own env.step loops in wall
+    time, so an oversubscribed share is not overstated); per_gpu_share = value / the node's GPUs (the
+    host cores split evenly over them).  ECO_CPU_BASELINE_PROCS caps the process count (testing)."""
     import subprocess
     try:
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count() or 1
-    procs = max(1, min(share, int(os.environ.get("ECO_CPU_BASELINE_PROCS", "16"))))
+    cap = int(os.environ.get("ECO_CPU_BASELINE_PROCS", "0")) or share
+    procs = max(1, min(share, cap))
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, "-m", "oracle.refcost", str(n), str(seconds), str(100 + i)], cwd=REPO,
                            env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
@@ -126,7 +129,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0):
         pass
     return dict(value=float(sum(rates)), unit="env-steps/s", cores=procs, kind="port",
                 nproc=os.cpu_count(), cpu_share=share, cpu_model=_cpu_model(),
-                per_core=float(np.mean(rates)),
+                per_core=float(np.mean(rates)), gpus_on_node=gpus_on_node,
+                per_gpu_share=float(sum(rates)) / max(1, gpus_on_node),
                 sample=f"{steps} ER-{n} env.step calls (random actions, T=2N episodes) in {procs} single-threaded "
                        f"processes x {seconds:.0f}s of oracle/refcost.py, the reference-cost restatement of "
                        "spinsystem.py:355-574",
@@ -194,6 +198,36 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
         return bw["hbm_bytes_per_launch"] + wg["hbm_bytes_per_launch"]
     except (KeyError, StopIteration):
         return None
+
+
+def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234):
+    """The batched MaxCut env step kernel alone (spinsystem.py:355-559, ER(n, 0.15) +-1 graphs, one per
+    episode, uniform random actions drawn beforehand): env-steps/s over `steps` launches timed with HIP
+    events on the launch stream, and the mean launch time (ms)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget
+    store = GraphStore.random("ER", B, n, 0.15, seed=seed, device=dev)
+    T = 2 * n
+    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        norm_rewards=True, basin_reward=1. / n)
+    steps = min(steps, T - warmup)
+    g = torch.Generator(device=dev).manual_seed(7)
+    acts = torch.randint(0, n, (warmup + steps, B), generator=g, device=dev, dtype=torch.int32)
+    env.reset(graph_ids=np.arange(B), seed=seed)
+    for i in range(warmup):
+        env.step(acts[i])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(steps):
+        env.step(acts[warmup + i])
+    e1.record()
+    torch.cuda.synchronize()
+    env.check_errors()
+    ms = e0.elapsed_time(e1) / steps
+    return B / (ms * 1e-3), ms
 
 
 def _free_port():
@@ -453,12 +487,21 @@ def main():
                                    bf16_peak=BF16_MFMA_PEAK_TFLOPS, bf16_frac=issued / BF16_MFMA_PEAK_TFLOPS,
                                    mfma_source=mf["source"])
         if not args.no_cpu_baseline and world == 1:
-            if args.graph == "ER":
-                out["cpu_baseline"] = cpu_refcost_baseline(n)
-                out["vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
-                out["vs_cpu_baseline_note"] = ("GPU full train loop (act + env step + replay + 8 gradient steps) "
-                                               "over the CPU reference-cost env step alone (no network, no training)")
             out["cpu_baseline_learn_loop"] = cpu_baseline(n, train=train)
+            if args.graph == "ER":
+                es_rate, es_ms = envstep_rate(dev, B, n)
+                out["cpu_baseline"] = cpu_refcost_baseline(n, gpus_on_node=torch.cuda.device_count())
+                cb = out["cpu_baseline"]
+                # like for like: env step vs env step (rollout, random policy) and learn loop vs learn loop
+                out["vs_cpu_baseline"] = {
+                    "env_step": {"gpu_env_step_kernel": es_rate, "gpu_kernel_ms": es_ms,
+                                 "cpu_all_cores": cb["value"], "ratio": es_rate / cb["value"],
+                                 "ratio_vs_per_gpu_share": es_rate / cb["per_gpu_share"]},
+                    "learn_loop": {"gpu_train_loop": value, "cpu_learn_loop": out["cpu_baseline_learn_loop"]["value"],
+                                   "ratio": value / out["cpu_baseline_learn_loop"]["value"]},
+                    "note": "env_step: the batched env step kernel alone (ER-%d x %d, random actions, HIP events) "
+                            "over the reference-cost env.step on every host core; learn_loop: this line's value "
+                            "over the oracle learn loop (act + env.step + train_step(64)/32 steps) on the host" % (n, B)}
         print(json.dumps(out))
     if dist:
         torch.distributed.destroy_process_group()

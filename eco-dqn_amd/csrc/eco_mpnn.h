@@ -46,7 +46,25 @@ constexpr int BF_TOTAL = BFT_LAYER + 3 * BF_LAYER_STRIDE;  // bf16 elements
 // node-feature columns 8..15 (n_obs_in > 8, MAIN_OBSERVABLES): W0 [64][8] and Wx [64][8] (row 63 zero)
 constexpr int PK_W0H = (PK_BF + BF_TOTAL / 2 + 3) & ~3;
 constexpr int PK_WXH = PK_W0H + 512;
-constexpr int PK_TOTAL = PK_WXH + 512;
+// fp16x2 pieces of the dense-path Linears (eco_mpnn_dense2.h): every Linear scaled by a power of two 2^kw
+// (kw per matrix, from its max |w|, into [2^14, 2^15)) and split W s = W1 + W2 with W1 = fp16(W s) and
+// W2 = fp16(W s - W1) (round to nearest): 22 significand bits, representation error <= 2^-22 |w| (or
+// 2^-39 max|W| for entries 2^17 below the matrix maximum).  Same fragment geometry as the bf16 pieces
+// ([half][piece p][nt][kc2], 64 lanes x 8 fp16, bf16_kprime_feature order), two pieces per half.
+// PK_FHS: the exponents kw as int32 bits, in the order Wf, (Wm, Wu) x 3 layers.
+constexpr int PK_FHS = PK_WXH + 512;
+constexpr int FH_NMAT = 7;
+constexpr int PK_FH = PK_FHS + 8;
+constexpr int FH_FRAG = 512;                         // fp16 per fragment (1 KB)
+constexpr int FH_HALF = 2 * 4 * 2 * FH_FRAG;         // one 64-input half (16 fragments, 16 KB)
+constexpr int FH_WF = 0;
+constexpr int FH_LAYER = FH_HALF;                    // + l * FH_LAYER_STRIDE: message (2 halves), update (2)
+constexpr int FH_LAYER_STRIDE = 4 * FH_HALF;
+constexpr int FH_FWD_END = FH_LAYER + 3 * FH_LAYER_STRIDE;
+constexpr int FHT_WF = FH_FWD_END;                   // transposed (backward), as BFT_*
+constexpr int FHT_LAYER = FHT_WF + FH_HALF;
+constexpr int FH_TOTAL = FHT_LAYER + 3 * FH_LAYER_STRIDE;  // fp16 elements
+constexpr int PK_TOTAL = PK_FH + FH_TOTAL / 2;
 
 // k' -> input feature of the bf16 Linear operands: within each 64-feature block, k' = 32kc + 8q + j
 // (kc = 0,1; q = lane >> 4; j = 0..7) holds feature 16(2kc + (j >> 2)) + 4q + (j & 3), i.e. the two

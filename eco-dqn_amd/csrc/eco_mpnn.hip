@@ -41,15 +41,74 @@ __device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
 
 }  // namespace eco
 #include "eco_mpnn_dense.h"  // dense-aggregation kernels (after the phase-timing buffer)
+#include "eco_mpnn_dense2.h"  // their fp16x2 successors
 #include "eco_mpnn_shared.h"  // many episodes on one shared large graph (G22)
 namespace eco {
+
+// Per-matrix power-of-two scale of the fp16x2 Linear pieces (PK_FHS, eco_mpnn.h): one block per matrix
+// (Wf, then Wm / Wu of each layer); kw puts max |w| 2^kw into [2^14, 2^15).
+__global__ __launch_bounds__(256) void pack_scale_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
+  const FlatOffsets o = flat_offsets(nobs);
+  const int m = blockIdx.x;
+  const float* W = m == 0 ? f + o.Wf : f + o.L + (m - 1) * 8192;
+  const int n = m == 0 ? 4096 : 8192;
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) mx = fmaxf(mx, fabsf(W[i]));
+  __shared__ float red[256];
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float v = red[0];
+    const int kw = (v > 0.f && v < INFINITY) ? 15 - __builtin_amdgcn_frexp_expf(v) : 0;
+    p[PK_FHS + m] = __int_as_float(kw);
+  }
+}
 
 __global__ void pack_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= PK_TOTAL) return;
   const FlatOffsets o = flat_offsets(nobs);
   float v = 0.f;
-  if (i >= PK_W0H) {  // feature columns 8..15
+  if (i >= PK_FHS && i < PK_FH) return;  // scale exponents: pack_scale_kernel
+  if (i >= PK_FH) {  // fp16x2 pieces, two fp16 per float slot
+    uint16_t h[2];
+    for (int t = 0; t < 2; ++t) {
+      const int e = 2 * (i - PK_FH) + t;
+      const bool tr = e >= FH_FWD_END;
+      const int et = tr ? e - FH_FWD_END : e;
+      const float* W;
+      int in_dim, lin, mat;
+      if (et < FH_LAYER) {
+        W = f + o.Wf;
+        in_dim = 64;
+        lin = et;
+        mat = 0;
+      } else {
+        const int e2 = et - FH_LAYER;
+        const int l = e2 / FH_LAYER_STRIDE, r = e2 % FH_LAYER_STRIDE;
+        const int which = r / (2 * FH_HALF);
+        W = f + o.L + l * 16384 + which * 8192;
+        in_dim = 128;
+        lin = r % (2 * FH_HALF);
+        mat = 1 + 2 * l + which;
+      }
+      const int frag = lin / FH_FRAG, within = lin % FH_FRAG;
+      const int ln = within >> 3, jj = within & 7;
+      const int kc2 = frag & 1, nt = (frag >> 1) & 3, pl = (frag >> 3) & 1, half = frag >> 4;
+      const int kp = 64 * half + 32 * kc2 + 8 * (ln >> 4) + jj;
+      const float wv = tr ? W[bf16_kprime_feature(kp & 63) * in_dim + 64 * half + 16 * nt + (ln & 15)]
+                          : W[(16 * nt + (ln & 15)) * in_dim + bf16_kprime_feature(kp)];
+      const float s = ldexpf(wv, __float_as_int(p[PK_FHS + mat]));
+      const _Float16 h1 = (_Float16)s;
+      const _Float16 h2 = (_Float16)(s - (float)h1);
+      h[t] = __builtin_bit_cast(uint16_t, pl == 0 ? h1 : h2);
+    }
+    v = __uint_as_float((uint32_t)h[0] | ((uint32_t)h[1] << 16));
+  } else if (i >= PK_W0H) {  // feature columns 8..15
     const bool wx = i >= PK_WXH;
     const int j = i - (wx ? PK_WXH : PK_W0H);
     const int r = j >> 3, c = 8 + (j & 7);
@@ -1005,6 +1064,7 @@ extern "C" size_t eco_mpnn_packed_count(void) { return (size_t)PK_TOTAL; }
 extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packed, eco_stream_t stream) {
   if (!params || !packed) return fail(ECO_ERR_ARG, "null params/packed");
   if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 16]");
+  pack_scale_kernel<<<FH_NMAT, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   pack_kernel<<<(PK_TOTAL + 255) / 256, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   return check_launch("mpnn_pack");
 }
@@ -1103,8 +1163,10 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   if (norm_scope == ECO_NORM_PER_CALL) {
     call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
-  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE"))
-    return mpnn_forward_dense_launch(a, saved != nullptr, st);
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) {
+    static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernel
+    return v1 ? mpnn_forward_dense_launch(a, saved != nullptr, st) : mpnn_forward_dense2_launch(a, saved != nullptr, st);
+  }
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
     // one graph shared by every episode (GSet best-cut search): node-major episode-batched kernels

@@ -1,0 +1,542 @@
+// Dense-aggregation MPNN forward on fp16x2 operands (src/networks/mpnn.py:40-159) for blocks of <= 224 rows
+// with +-1 edge weights (ER-20 ... ER-200): the successor of eco_mpnn_dense.h's bf16x3 kernel.
+//
+// Every MFMA operand that is not exactly representable is carried as TWO fp16 pieces of a power-of-two-scaled
+// value: v 2^k = V1 + V2, V1 = fp16(v 2^k), V2 = fp16(v 2^k - V1) (round to nearest, 22 significand bits:
+// representation error <= 2^-22 |v|), on v_mfma_f32_16x16x32_f16 with f32 accumulation.  The scale 2^k puts the
+// operand's block maximum into [2^14, 2^15), inside fp16's normal range whatever the magnitudes (activations of a
+// std-0.01 network fall by ~10x per layer).  Against the bf16x3 forms of eco_mpnn_dense.h this needs 2/3 of the
+// aggregation MFMAs and LDS reads (two planes instead of three) and half of the Linear MFMAs (three products
+// W1.X1 + W1.X2 + W2.X1 instead of six).  The dropped W2.X2 is 2^-22 of the largest product; measured against
+// float64 the products are closer than torch's own fp32 matmul (tools: /tmp f16 emulation in DESIGN.md §5).
+//
+//   * Aggregation agg[f][i] = sum_j H[j][f] A[j][i]: the planes hold H of tile t (16 rows) scaled by 2^k_t (k_t
+//     from the tile's max |h|, written by the wave that owns the tile next to its planes); the adjacency operand,
+//     built in registers from bitmasks, carries +-2^(c - k_t) instead of +-1 (exact in fp16 for
+//     c - k_t in [-24, 15]; c = 15 + min_t k_t per aggregation), so every product is h 2^c and the f32 sum is
+//     scaled back by 2^-c -- folded into the 1/norm multiply.  Rows of a tile more than 2^39 below the block's
+//     largest tile get a zero operand (they contribute < 2^-39 of the largest term).
+//   * Linears: weights pre-split per matrix (PK_FH, scale 2^kw); activations scaled per node by 2^kx (node max
+//     over the Linear's 64 or 128 inputs: four lanes hold one node, combined with permlane swaps), unscaled by
+//     2^-(kx + kw) after the f32 accumulation.
+//
+// One 1024-thread workgroup (16 waves) per block of whole graphs, wave w owns 16-node tile w (h and e in
+// registers), as eco_mpnn_dense.h.  LDS keeps a whole layer's weights resident (three rotating 32-KB buffers:
+// message and update Linear of the layer + the next layer's message Linear prefetched by LDS-DMA), so a layer
+// has two barriers (planes ready -> aggregation; aggregation done + weights landed -> Linears -> next planes)
+// instead of four; the edge layer writes the U and V planes at once (V into the two idle weight buffers).
+// Saved activations and ReLU masks have the layout of eco_mpnn_dense.h (the backward reads them unchanged).
+#pragma once
+#include "eco_mpnn_dense.h"
+
+namespace eco {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int D2_PLANE = 4 * DN_KPMAX * 16;           // fp16 per plane: [4 feature blocks][224 rows][16]
+constexpr int D2_PL_BYTES = 2 * D2_PLANE * 2;          // two planes: 57,344 B
+constexpr int D2_WBUF = 2 * FH_HALF;                   // fp16 per weight buffer: one 128-input Linear (32 KB)
+constexpr int D2_WBUF_BYTES = D2_WBUF * 2;
+constexpr int D2_TE_INTS = 32;                         // tile exponents: [0..15] current planes, [16..31] V planes
+constexpr int D2_K_EMPTY = 127;                        // tile exponent of an all-zero tile
+
+inline size_t dense2_fwd_lds_bytes(int rows_pad, int gpb) {
+  return (size_t)D2_PL_BYTES + 3 * D2_WBUF_BYTES + D2_TE_INTS * 4 + (size_t)rows_pad * 8 + (size_t)gpb * 12 + 16;
+}
+
+// ---- fp16x2 splitting -------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+  const f32x2v v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));  // v_cvt_pk_f16_f32 (RNE)
+}
+// (a, b) already scaled into fp16 range -> hi and lo fp16 pairs with a = hi + lo to 2^-22
+__device__ __forceinline__ void split2_pk(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pk_f16(a, b);
+  const f32x2v back = __builtin_convertvector(__builtin_bit_cast(f16x2v, hi), f32x2v);
+  const f32x2v v = {a, b};
+  const f32x2v r = v - back;  // exact (Sterbenz / subnormal remainder)
+  lo = pk_f16(r[0], r[1]);
+}
+// 2^k as a float (k clamped to the normal range)
+__device__ __forceinline__ float exp2i(int k) {
+  k = k < -126 ? -126 : (k > 127 ? 127 : k);
+  return __int_as_float((k + 127) << 23);
+}
+
+// wave-wide max of non-negative floats (DPP row rotations, then across rows with permlane swaps)
+__device__ __forceinline__ float wave_max_nonneg(float m) {
+  int v = __float_as_int(m);
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x122, 0xF, 0xF, false));  // row_ror:2
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x121, 0xF, 0xF, false));  // row_ror:1
+  auto s16 = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = max((int)s16[0], (int)s16[1]);
+  auto s32 = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  return __int_as_float(max((int)s32[0], (int)s32[1]));  // non-negative floats order as ints
+}
+// max over the four lanes l, l^16, l^32, l^48 (one node of the node-operand layout) of a non-negative float
+__device__ __forceinline__ float node_max_nonneg(float m) {
+  auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  const float a = fmaxf(__uint_as_float(s16[0]), __uint_as_float(s16[1]));
+  auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+  return fmaxf(__uint_as_float(s32[0]), __uint_as_float(s32[1]));
+}
+// scale exponent k with max 2^k in [2^14, 2^15) (0 for an all-zero / non-finite max)
+__device__ __forceinline__ int scale_exp(float mx) {
+  if (!(mx > 0.f) || mx == INFINITY) return 0;
+  int k = 15 - __builtin_amdgcn_frexp_expf(mx);
+  return k < -110 ? -110 : (k > 110 ? 110 : k);
+}
+__device__ __forceinline__ float absmax4(const float4& v, float m) {
+  return fmaxf(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))), m);
+}
+
+// 8 activations (float4 c = 2kc2, 2kc2+1 of a 64-input half) scaled by sf, as hi / lo fp16 B fragments
+__device__ __forceinline__ void split_fh(const float4& a, const float4& b, float sf, f16x8& hi, f16x8& lo) {
+  uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
+  split2_pk(a.x * sf, a.y * sf, h0, l0);
+  split2_pk(a.z * sf, a.w * sf, h1, l1);
+  split2_pk(b.x * sf, b.y * sf, h2, l2);
+  split2_pk(b.z * sf, b.w * sf, h3, l3);
+  const u32x4v h = {h0, h1, h2, h3}, l = {l0, l1, l2, l3};
+  hi = __builtin_bit_cast(f16x8, h);
+  lo = __builtin_bit_cast(f16x8, l);
+}
+
+// acc[nt] += W[16nt + .][one 64-input half] . x for x = hi + lo (split_fh of the half's four float4), three
+// products (smallest first).  WH: the half's 16 fragments [p][nt][kc2] in LDS.
+__device__ __forceinline__ void mm_fh(f32x4 (&acc)[4], const float4 (&x)[4], float sf, const uint16_t* WH, int lane) {
+  const uint16_t* wl = WH + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 xh, xl;
+    split_fh(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f16x8 w1 = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      const f16x8 w2 = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
+    }
+  }
+}
+
+// node scale of a Linear's inputs (the lane's float4s of every half)
+template <int NC>
+__device__ __forceinline__ int node_exp(const float4 (&x)[NC]) {
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) m = absmax4(x[c], m);
+  return scale_exp(node_max_nonneg(m));
+}
+__device__ __forceinline__ int node_exp2(const float4 (&x)[4], const float4 (&y)[4]) {
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) m = absmax4(y[c], absmax4(x[c], m));
+  return scale_exp(node_max_nonneg(m));
+}
+__device__ __forceinline__ void unscale(f32x4 (&acc)[4], int k) {
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[nt][i] = __builtin_ldexpf(acc[nt][i], -k);
+}
+__device__ __forceinline__ int fh_kw(const float* P, int m) { return __float_as_int(P[PK_FHS + m]); }
+
+// ---- planes ---------------------------------------------------------------------------------------------------
+// tile scale exponent of the wave's 16 nodes x 64 features (identical in every lane; D2_K_EMPTY for all zero)
+__device__ __forceinline__ int tile_exp(const float4 (&v)[4]) {
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) m = absmax4(v[c], m);
+  const float mx = wave_max_nonneg(m);
+  return mx > 0.f ? scale_exp(mx) : D2_K_EMPTY;
+}
+// features 16ft + 4k .. +3 of node j, already scaled, as two fp16 planes
+__device__ __forceinline__ void plane2_store4(uint16_t* PL, int ft, int j, int k, float4 v) {
+  uint32_t h0, l0, h1, l1;
+  split2_pk(v.x, v.y, h0, l0);
+  split2_pk(v.z, v.w, h1, l1);
+  const int o = plane_off(ft, j, k);
+  *reinterpret_cast<uint2*>(PL + o) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(PL + D2_PLANE + o) = make_uint2(l0, l1);
+}
+// the tile's four float4 (node-operand layout) scaled by 2^k into the planes; lane 0 records k in TE[tile]
+__device__ __forceinline__ void tile_planes(uint16_t* PL, int* TE, int tile, int r, int s4, const float4 (&v)[4],
+                                            int lane) {
+  const int k = tile_exp(v);
+  const float sf = exp2i(k == D2_K_EMPTY ? 0 : k);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    plane2_store4(PL, c, r, s4, make_float4(v[c].x * sf, v[c].y * sf, v[c].z * sf, v[c].w * sf));
+  if (lane == 0) TE[tile] = k;
+}
+
+// Per aggregation: from the tile exponents TE[0 .. ntiles) -> c (products are h 2^c) and, per tile t, the fp16
+// pattern of the adjacency magnitude 2^(c - k_t) replicated in both halves of a dword (0: dropped / empty tile).
+// Lane t < 16 works on tile t; the caller reads pattern t with readlane.
+struct AggScale {
+  uint32_t pat;  // lane t: pattern of tile t
+  int c;
+};
+__device__ __forceinline__ AggScale agg_scale(const int* TE, int ntiles, int lane) {
+  const int t = lane & 15;
+  const int k = t < ntiles ? TE[t] : D2_K_EMPTY;
+  int kmin = k;  // min over the row (lanes 0..15 hold tiles 0..15)
+  kmin = min(kmin, __builtin_amdgcn_update_dpp(kmin, kmin, 0x128, 0xF, 0xF, false));
+  kmin = min(kmin, __builtin_amdgcn_update_dpp(kmin, kmin, 0x124, 0xF, 0xF, false));
+  kmin = min(kmin, __builtin_amdgcn_update_dpp(kmin, kmin, 0x122, 0xF, 0xF, false));
+  kmin = min(kmin, __builtin_amdgcn_update_dpp(kmin, kmin, 0x121, 0xF, 0xF, false));
+  kmin = __builtin_amdgcn_readfirstlane(kmin);
+  AggScale s;
+  s.c = kmin == D2_K_EMPTY ? 0 : 15 + kmin;
+  const int E = s.c - k;  // <= 15 by the choice of c
+  uint32_t p = 0u;
+  if (k != D2_K_EMPTY) p = E >= -14 ? (uint32_t)(E + 15) << 10 : (E >= -24 ? 1u << (E + 24) : 0u);
+  s.pat = p | (p << 16);
+  return s;
+}
+
+// the lane's adjacency bits of k-chunk kc (adj_bits16: nz byte, neg byte, element jj <-> bit jj) spread for the
+// fragment builder: nz of elements 0,2,4,6 -> bits 0..3, neg of them -> 4..7, nz of 1,3,5,7 -> 16..19, neg -> 20..23
+__device__ __forceinline__ uint32_t adj_spread(uint32_t b16) {
+  uint32_t e = b16 & 0x5555u, o = (b16 >> 1) & 0x5555u;
+  e = (e | (e >> 1)) & 0x3333u;
+  e = (e | (e >> 2)) & 0x0F0Fu;
+  o = (o | (o >> 1)) & 0x3333u;
+  o = (o | (o >> 2)) & 0x0F0Fu;
+  return ((e | (e >> 4)) & 0xFFu) | (((o | (o >> 4)) & 0xFFu) << 16);
+}
+// B fragment (8 fp16 adjacency entries of the lane's node for the chunk's k slots) from a spread word; PPlo / PPhi:
+// magnitude patterns of the chunk's two tiles.  MODE 0: A (signed); 1: A+ = [A = +1]; 2: A- = [A = -1] as +1.
+template <int MODE>
+__device__ __forceinline__ f16x8 adj_frag2(uint32_t W, uint32_t PPlo, uint32_t PPhi) {
+  u32x4v d;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t PP = t < 2 ? PPlo : PPhi;
+    const uint32_t nz = (W >> t) & 0x10001u, ng = (W >> (t + 4)) & 0x10001u;
+    const uint32_t on = MODE == 0 ? nz : (MODE == 1 ? (nz & ~ng) : ng);
+    uint32_t v = (on * 0xFFFFu) & PP;
+    if (MODE == 0) v |= ng << 15;
+    d[t] = v;
+  }
+  return __builtin_bit_cast(f16x8, d);
+}
+
+// acc[ft] += sum over chunks kc in [kc0, kc1) and both planes of Hs[j][16ft + ..] . B[j][node] (products h 2^c);
+// adjw[kc]: spread adjacency words; sc: agg_scale of the planes.  EXEC all ones (wave-uniform branches only).
+template <int MODE>
+__device__ __forceinline__ void agg2(f32x4 (&acc)[4], const uint16_t* PL, const uint32_t (&adjw)[DN_KC],
+                                     const AggScale& sc, int kc0, int kc1, int lane) {
+  const int q = lane >> 4;
+  const int j_in = 4 * q + ((lane >> 2) & 3);
+  const int pc = (lane & 3) ^ q;
+#pragma unroll
+  for (int kc = 0; kc < DN_KC; ++kc) {
+    if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
+    const uint32_t plo = __builtin_amdgcn_readlane(sc.pat, 2 * kc);
+    const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
+    const f16x8 bf = adj_frag2<MODE>(adjw[kc], plo, phi);
+    const uint16_t* base = PL + (32 * kc + j_in) * 16 + 4 * pc;
+#pragma unroll
+    for (int p = 1; p >= 0; --p) {  // the small plane first
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        const uint16_t* a = base + p * D2_PLANE + ft * (DN_KPMAX * 16);
+        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
+        const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const f16x8 af = __builtin_bit_cast(f16x8, raw);
+        acc[ft] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc[ft], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound the plane reads in flight (16-wave VGPR budget)
+  }
+}
+
+// zero the plane rows [rows_pad, KP) (read as zeros by the last k-chunk; no tile writes them)
+template <int NT>
+__device__ __forceinline__ void zero_pad_rows2(uint16_t* PL, int rows_pad) {
+  const int KP = (rows_pad + 31) & ~31;
+  for (int i = threadIdx.x; i < (KP - rows_pad) * 2 * 4 * 4; i += NT) {
+    const int k = i & 3, ft = (i >> 2) & 3, p = (i >> 4) & 1, j = rows_pad + (i >> 5);
+    *reinterpret_cast<uint2*>(PL + p * D2_PLANE + plane_off(ft, j, k)) = make_uint2(0u, 0u);
+  }
+}
+
+// LDS: PL 2 fp16 planes | WB0 | WB1 | WB2 (32 KB each: Linear fragments; WB1..WB2 hold the V planes of the edge
+//      layer, the readout uses PL..WB0 for fp32 h3 rows and WB1 as scratch) | TE [32] | RI [rows_pad] | GB | MD
+template <bool SAVE>
+__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(MpnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(0);
+  constexpr int NW = DN_NW;
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
+  uint16_t* WB0 = PL + 2 * D2_PLANE;
+  uint16_t* WB1 = WB0 + D2_WBUF;
+  uint16_t* WB2 = WB1 + D2_WBUF;
+  uint16_t* VPL = WB1;  // V planes of the edge layer (57,344 B of WB1..WB2)
+  int* TE = reinterpret_cast<int*>(WB2 + D2_WBUF);
+  int2* RI = reinterpret_cast<int2*>(TE + D2_TE_INTS);
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  int* MD = reinterpret_cast<int*>(GB + a.gpb);
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);  // [rows_pad][DN_ADJW] while a bitmask is built
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+
+  const bool has_tile = w < ntiles;
+  const int r = w * 16 + c16;
+  const bool valid = has_tile && r < rows_valid;
+  float xk0 = 0.f, xk1 = 0.f;
+  if (valid) {
+    xk0 = a.x[(R0 + r) * 8 + s4];
+    xk1 = a.x[(R0 + r) * 8 + 4 + s4];
+  }
+  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree ----
+  glds_frags<NW>(WB0, PH + FH_WF, 16, w, lane);
+  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
+    const int gid = a.gids[blk * a.gpb + gl];
+    GB[gl] = a.gs.edge_base[gid];
+    MD[gl] = a.gs.max_deg[gid];
+  }
+  __syncthreads();
+  ECO_TS(1);
+  const int rr = min(r, rows_pad - 1);
+  const RowInfo ri = row_info(RI, rr);
+  const float nf = (float)ri.norm;
+  const float rnf = 1.f / nf;
+  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  uint32_t adjw[DN_KC];
+  {
+    uint32_t adjb[4];
+    dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
+#pragma unroll
+    for (int kc = 0; kc < DN_KC; ++kc) adjw[kc] = adj_spread((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+  }
+  zero_pad_rows2<NT>(PL, rows_pad);
+  zero_pad_rows2<NT>(VPL, rows_pad);
+  auto wa_of = [&](int c) { return f4(P + PK_WA + 16 * c + 4 * s4); };
+
+  // ---- phase A: Z = Wx . x (f32 MFMA); U = relu(Z + w_a) and V = relu(Z - w_a) planes ----
+  if (has_tile) {
+    f32x4 z[4];
+    lin8(z, P + PK_WX, xk0, xk1, lane);
+    float4 u[4], v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 wa = wa_of(c);
+      u[c] = valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
+                                 relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
+                   : zero4();
+      v[c] = valid ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
+                                 relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
+                   : zero4();
+    }
+    tile_planes(PL, TE, w, r, s4, u, lane);
+    tile_planes(VPL, TE + 16, w, r, s4, v, lane);
+  }
+  glds_wait();  // Wf fragments
+  __syncthreads();
+  ECO_TS(2);
+
+  // ---- phase B: edge embedding (mpnn.py:89-104): (A+ . relu(Z + w_a) + A- . relu(Z - w_a)) / norm; Wf ----
+  float4 ereg[4];
+  {
+    const AggScale su = agg_scale(TE, ntiles, lane);
+    const AggScale sv = agg_scale(TE + 16, ntiles, lane);
+    f32x4 ea[4], ev[4];
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft) ea[ft] = ev[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) {
+      agg2<1>(ea, PL, adjw, su, kc0, kc1, lane);
+      agg2<2>(ev, VPL, adjw, sv, kc0, kc1, lane);
+    }
+    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
+    float4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float t4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        t4[i] = (__builtin_ldexpf(ea[c][i], -su.c) + __builtin_ldexpf(ev[c][i], -sv.c)) * rnf;
+      acc[c] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+    }
+    // feature 63 = norm / norm.max()  (mpnn.py:102)
+    const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? MD[r / N] : 1);
+    if (s4 == 3) acc[3].w = nf / (float)md;
+    if (!valid) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = zero4();
+    } else if (SAVE) {
+      float* eap = a.sv + (size_t)SV_EAGG * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(eap + 16 * c, acc[c]);
+    }
+    f32x4 d[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kx = node_exp<4>(acc);
+    if (has_tile) mm_fh(d, acc, exp2i(kx), WB0, lane);
+    unscale(d, kx + fh_kw(P, 0));
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      ereg[nt] = relu4(d[nt]);
+      if (SAVE && valid) st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, ereg[nt]);
+    }
+    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_E, pos_mask(ereg));
+  }
+  __syncthreads();  // every wave is done with the U / V planes and with Wf
+  ECO_TS(3);
+  // layer weights: Wm0 -> WB1, Wu0 -> WB2, Wm1 -> WB0 (landed by layer 0's first barrier)
+  glds_frags<NW>(WB1, PH + FH_LAYER, 32, w, lane);
+  glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_HALF, 32, w, lane);
+  glds_frags<NW>(WB0, PH + FH_LAYER + FH_LAYER_STRIDE, 32, w, lane);
+
+  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55), in registers + planes ----
+  float4 hreg[4];
+  {
+    f32x4 z[4];
+    lin8(z, P + PK_W0, xk0, xk1, lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      hreg[c] = valid ? relu4(z[c]) : zero4();
+      if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
+    }
+    if (has_tile) tile_planes(PL, TE, w, r, s4, hreg, lane);
+  }
+  if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H0, pos_mask(hreg));
+  __syncthreads();
+  ECO_TS(4);
+
+  // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
+  // per layer: [planes h_l + TE ready] (DMA of later weights) aggregation | wait + [B1] message, update (both
+  //            Linears resident), h' planes | [B2]
+  for (int layer = 0; layer < 3; ++layer) {
+    const uint16_t* WM = layer == 0 ? WB1 : (layer == 1 ? WB0 : WB2);
+    const uint16_t* WU = layer == 0 ? WB2 : (layer == 1 ? WB1 : WB0);
+    if (layer == 1) {
+      glds_frags<NW>(WB1, PH + FH_LAYER + FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu1
+      glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_LAYER_STRIDE, 32, w, lane);            // Wm2
+    } else if (layer == 2) {
+      glds_frags<NW>(WB0, PH + FH_LAYER + 2 * FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu2
+    }
+    const AggScale sh = agg_scale(TE, ntiles, lane);
+#pragma unroll
+    for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[kc]));  // no hoisting of the 56 fragment masks
+    f32x4 ag[4];
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) agg2<0>(ag, PL, adjw, sh, kc0, kc1, lane);
+    float4 agg[4];
+    {
+      const float sc = __builtin_ldexpf(rnf, -sh.c);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) agg[c] = make_float4(ag[c][0] * sc, ag[c][1] * sc, ag[c][2] * sc, ag[c][3] * sc);
+    }
+    if (SAVE && valid) {
+      float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
+    }
+    glds_wait();
+    __syncthreads();  // B1: planes read by every wave; this layer's weights landed
+    // message = relu(Wm . [agg, e])
+    float4 mrel[4];
+    {
+      f32x4 d[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kx = node_exp2(agg, ereg);
+      const float sf = exp2i(kx);
+      if (has_tile) {
+        mm_fh(d, ereg, sf, WM + FH_HALF, lane);
+        mm_fh(d, agg, sf, WM, lane);
+      }
+      unscale(d, kx + fh_kw(P, 1 + 2 * layer));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) mrel[c] = relu4(d[c]);
+    }
+    if (SAVE && valid) {
+      float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
+      store_mask(a, RT, R0 + r, s4, SM_M0 + layer, pos_mask(mrel));
+    }
+    // h' = relu(Wu . [h, m])
+    {
+      f32x4 hn[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kx = node_exp2(hreg, mrel);
+      const float sf = exp2i(kx);
+      if (has_tile) {
+        mm_fh(hn, hreg, sf, WU, lane);
+        mm_fh(hn, mrel, sf, WU + FH_HALF, lane);
+      }
+      unscale(hn, kx + fh_kw(P, 2 + 2 * layer));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        hreg[c] = valid ? relu4(hn[c]) : zero4();
+        if (SAVE && valid) st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
+      }
+    }
+    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H1 + layer, pos_mask(hreg));
+    if (layer < 2 && has_tile) tile_planes(PL, TE, w, r, s4, hreg, lane);
+    __syncthreads();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
+    ECO_TS(5 + layer);
+  }
+
+  // ---- phase E: readout + act over h3 rows staged as fp32 [rows][LDH] (planes + WB0 region) ----
+  float* Hs = lds;
+  if (has_tile) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st4(Hs + r * LDH + 16 * c + 4 * s4, hreg[c]);
+  }
+  __syncthreads();
+  float* Scr = reinterpret_cast<float*>(WB1);
+  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= 2 * D2_WBUF_BYTES;
+  readout_act<SAVE, NW>(a, Hs, LDH, Scr, split, blk, g_valid, rows_valid, R0, RT);
+  ECO_TS(8);
+}
+
+static int mpnn_forward_dense2_launch(const MpnnArgs& a, bool save, hipStream_t st) {
+  const int rows_pad = (a.gpb * a.N + 15) & ~15;
+  const size_t lds = dense2_fwd_lds_bytes(rows_pad, a.gpb);
+  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
+  if ((size_t)rows_pad * LDH * 4 > (size_t)D2_PL_BYTES + D2_WBUF_BYTES)  // h3 rows must end before WB1
+    return fail(ECO_ERR_ARG, "dense MPNN readout rows exceed the plane + buffer region");
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  if (save) {
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    mpnn_forward_dense2_kernel<true><<<blocks, 64 * DN_NW, lds, st>>>(a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense2_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    mpnn_forward_dense2_kernel<false><<<blocks, 64 * DN_NW, lds, st>>>(a);
+  }
+  return check_launch("mpnn_forward_dense2");
+}
+
+}  // namespace eco

@@ -2,7 +2,9 @@
 rehearsal of the RCCL path the driver's multi-GPU bench takes), each with its own graphs, episodes, replay
 and seed.  After a short learn() the parameters must be bitwise identical on every rank (one flat gradient
 all-reduce per optimiser step, the mean folded into Adam), must have moved from the broadcast initial
-weights, and every rank must have taken the same number of gradient steps."""
+weights, and every rank must have taken the same number of gradient steps.  The worker also checks the
+exchange of the first three gradient steps: reduced buffer == rank-order sum of the local gradients, scale
+1/world, and Adam's first moment moved by (1 - beta1)(mean gradient - m) (see dist_train_worker.py)."""
 import os
 import socket
 import subprocess
@@ -38,6 +40,8 @@ def test_two_ranks_train_to_identical_parameters():
             raise
         outs.append(out)
         assert p.returncode == 0, out[-3000:]
+    ex = next(l for l in outs[0].splitlines() if l.startswith("EXCHANGE_OK")).split()
+    assert int(ex[1]) == 3 and float(ex[2]) < 1e-5
     line = next(l for l in outs[0].splitlines() if l.startswith("DIST_OK"))
     parts = line.split(maxsplit=5)
     steps, diff, init_same, moved = int(parts[1]), float(parts[2]), float(parts[3]), float(parts[4])
