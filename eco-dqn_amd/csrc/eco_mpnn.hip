@@ -1222,7 +1222,10 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.sv = (float*)saved;
   a.dq = dq;
   a.gr = (float*)gradws;
-  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dense_launch(a, st);
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) {
+    static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernels
+    return v1 ? mpnn_backward_dense_launch(a, st) : mpnn_backward_dense2_launch(a, st);
+  }
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");

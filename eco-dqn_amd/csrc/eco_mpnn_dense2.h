@@ -539,4 +539,364 @@ static int mpnn_forward_dense2_launch(const MpnnArgs& a, bool save, hipStream_t 
   return check_launch("mpnn_forward_dense2");
 }
 
+
+// Two output halves (fragment sets WH0, WH1) of one 64-input transposed Linear sharing the split of x.
+__device__ __forceinline__ void mm_fh2(f32x4 (&acc0)[4], f32x4 (&acc1)[4], const float4 (&x)[4], float sf,
+                                       const uint16_t* WH0, const uint16_t* WH1, int lane) {
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 xh, xl;
+    split_fh(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint16_t* wl = (hh ? WH1 : WH0) + lane * 8;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4& acc = hh ? acc1[nt] : acc0[nt];
+        const f16x8 w1 = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+        const f16x8 w2 = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight (register pressure at 16 waves)
+    }
+  }
+}
+
+// ============================================================== backward ====
+// Autograd of mpnn_forward_dense2_kernel (dqn.py:440-449) on the same fp16x2 operands: the A^T products are the
+// forward's scaled-plane aggregation over the gathered gradient G (A symmetric), the Linears transposed fp16x2
+// products (PK_FH transposed pieces, the matrix scales of the forward).  Writes the same pre-activation
+// gradients and per-graph / per-block partials as mpnn_backward_dense_kernel (the weight-gradient reduction is
+// shared).  A layer's two transposed Linears are resident (three rotating 32-KB buffers: Wu^T, Wm^T, and the next
+// layer's Wu^T prefetched), three barriers per layer (Wm^T landed | G planes ready | planes read).
+// LDS: PL 2 planes (readout scratch first) | WB0 | WB1 | WB2 | TE [16] | RI [rows_pad] int2 | GB [gpb] i64
+__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(MpnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_TS(16);
+  constexpr int NW = DN_NW;
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);
+  uint16_t* WB0 = PL + 2 * D2_PLANE;
+  uint16_t* WB1 = WB0 + D2_WBUF;
+  uint16_t* WB2 = WB1 + D2_WBUF;
+  int* TE = reinterpret_cast<int*>(WB2 + D2_WBUF);
+  int2* RI = reinterpret_cast<int2*>(TE + D2_TE_INTS);
+  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  const float* sv = a.sv;
+  float* gr = a.gr;
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
+  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
+  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
+  const float* PP = MEAN + (size_t)a.B * 64;
+  float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
+  float* DWRA = DP + (size_t)a.B * 64;
+  float* DWRB = DWRA + (size_t)a.B * 64;
+  float* DBR = DWRB + (size_t)a.B * 64;
+  float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
+  auto WUT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE + 2 * FH_HALF; };  // Wu^T: 2 output halves
+  auto WMT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE; };                // Wm^T: dagg, de halves
+
+  // ---- staging: Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (LDS-DMA), row info, edge bases ----
+  glds_frags<NW>(WB0, WUT(2), 32, w, lane);
+  glds_frags<NW>(WB1, WMT(2), 32, w, lane);
+  glds_frags<NW>(WB2, WUT(1), 32, w, lane);
+  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
+  for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
+  __syncthreads();
+  const bool has_tile = w < ntiles;
+  const int rw = w * 16 + c16;
+  const bool valid = has_tile && rw < rows_valid;
+  const int rr = min(rw, rows_pad - 1);
+  const float nf = (float)row_info(RI, rr).norm;
+  const float rnf = 1.f / nf;
+  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  uint32_t adjw[DN_KC];
+  {
+    uint32_t adjb[4];
+    dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, rw, rr, valid, s4, adjb);
+#pragma unroll
+    for (int kc = 0; kc < DN_KC; ++kc) adjw[kc] = adj_spread((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+  }
+  const uint16_t* Msk = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
+  const uint4 rmask = valid ? *reinterpret_cast<const uint4*>(Msk + ((R0 + rw) * 4 + s4) * SM_TENSORS)
+                            : make_uint4(0u, 0u, 0u, 0u);
+  ECO_TS(17);
+
+  // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
+  float* DQ = lds;                       // [rows_pad]
+  float* DMEAN = DQ + rows_pad;          // [gpb][64]
+  float* RED = DMEAN + a.gpb * 64;       // [gpb][NW][64] (split) or [NW][64]
+  const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)D2_PL_BYTES;
+  for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
+  __syncthreads();
+  if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
+    for (int gl = 0; gl < g_valid; ++gl) {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      float dwb = 0.f;
+      for (int v = w; v < N; v += NW) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+      RED[(gl * NW + w) * 64 + lane] = dwb;
+    }
+    __syncthreads();
+  }
+  for (int gl = w; gl < g_valid; gl += NW) {
+    const int e = blk * a.gpb + gl;
+    float sacc = 0.f;
+    for (int v = lane; v < N; v += 64) sacc += DQ[gl * N + v];
+    const float S = wave_sum_f(sacc);
+    const float p = PP[(size_t)e * 64 + lane];
+    const float dp = P[PK_WR + lane] * S * (p > 0.f ? 1.f : 0.f);
+    DP[(size_t)e * 64 + lane] = dp;
+    DWRA[(size_t)e * 64 + lane] = relu(p) * S;
+    if (lane == 0) DBR[e] = S;
+    float dmean = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
+    DMEAN[gl * 64 + lane] = dmean / (float)N;
+    float dwb = 0.f;
+    if (split) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) dwb += RED[(gl * NW + k) * 64 + lane];  // fixed order
+    } else {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      for (int v = 0; v < N; ++v) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+    }
+    DWRB[(size_t)e * 64 + lane] = dwb;
+  }
+  __syncthreads();
+  // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
+  float4 dh[4];
+  {
+    const float dqi = valid ? DQ[rw] : 0.f;
+    const int gl = rr / N;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 16 * c + 4 * s4;
+      const float4 dm = valid ? f4(DMEAN + gl * 64 + f) : zero4();
+      dh[c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
+                          fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
+    }
+  }
+  __syncthreads();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
+  zero_pad_rows2<NT>(PL, rows_pad);
+  ECO_TS(18);
+
+  // ---- update layers in reverse (mpnn.py:114-120) ----
+  // duu, [dh_direct, dm] = Wu^T . duu (resident), dum | wait + [B0] Wm^T landed; [dagg, de] = Wm^T . dum, G planes |
+  // [B1] dh = dh_direct + A.G | [B2] planes and this layer's buffers free: DMA of the next layers' weights
+  float4 de[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) de[c] = zero4();
+  for (int layer = 2; layer >= 0; --layer) {
+    const uint16_t* WU = layer == 2 ? WB0 : (layer == 1 ? WB2 : WB1);
+    const uint16_t* WM = layer == 2 ? WB1 : (layer == 1 ? WB0 : WB2);
+    const size_t ro = (R0 + rr) * 64 + 4 * s4;
+    // duu = dh' * [h' > 0]  (in place in dh)
+    {
+      const uint32_t hmask = mask16(rmask, SM_H0 + layer + 1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dh[c] = masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, hmask, c);
+        if (valid) st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[c]);
+      }
+    }
+    // [dh_direct, dm] = Wu^T . duu;  dum = dm * [m > 0]
+    f32x4 dhd[4];
+    float4 dum[4];
+    {
+      f32x4 dmm[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dhd[nt] = dmm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kx = node_exp<4>(dh);
+      if (has_tile) mm_fh2(dhd, dmm, dh, exp2i(kx), WU, WU + FH_HALF, lane);
+      const int ku = kx + fh_kw(P, 2 + 2 * layer);
+      unscale(dhd, ku);
+      unscale(dmm, ku);
+      const uint32_t mmask = mask16(rmask, SM_M0 + layer);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        dum[c] = masked(dmm[c], mmask, c);
+        if (valid) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
+      }
+    }
+    if (layer == 1) ECO_TS(24);
+    glds_wait();
+    __syncthreads();  // B0: Wm^T landed
+    if (layer == 1) ECO_TS(25);
+    // [dagg, de] = Wm^T . dum;  G = dagg / norm -> planes
+    {
+      f32x4 dg[4], dd[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dg[nt] = dd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kx = node_exp<4>(dum);
+      if (has_tile) mm_fh2(dg, dd, dum, exp2i(kx), WM, WM + FH_HALF, lane);
+      const int km = kx + fh_kw(P, 1 + 2 * layer);
+      unscale(dg, km);
+      unscale(dd, km);
+      float4 g[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        de[c].x += dd[c][0]; de[c].y += dd[c][1]; de[c].z += dd[c][2]; de[c].w += dd[c][3];
+        g[c] = valid ? make_float4(dg[c][0] * rnf, dg[c][1] * rnf, dg[c][2] * rnf, dg[c][3] * rnf) : zero4();
+      }
+      if (has_tile) tile_planes(PL, TE, w, rw, s4, g, lane);
+    }
+    if (layer == 1) ECO_TS(26);
+    __syncthreads();  // B1: G planes complete
+    if (layer == 1) ECO_TS(27);
+    // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
+    {
+      const AggScale sg = agg_scale(TE, ntiles, lane);
+#pragma unroll
+      for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[kc]));
+      f32x4 ag[4];
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (has_tile) agg2<0>(ag, PL, adjw, sg, kc0, kc1, lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float t4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t4[i] = dhd[c][i] + __builtin_ldexpf(ag[c][i], -sg.c);
+        dh[c] = valid ? make_float4(t4[0], t4[1], t4[2], t4[3]) : zero4();
+      }
+    }
+    if (layer == 1) ECO_TS(28);
+    __syncthreads();  // B2: planes read; this layer's buffers free
+    if (layer == 2) {
+      glds_frags<NW>(WB0, WMT(1), 32, w, lane);
+      glds_frags<NW>(WB1, WUT(0), 32, w, lane);
+    } else if (layer == 1) {
+      glds_frags<NW>(WB2, WMT(0), 32, w, lane);
+      glds_frags<NW>(WB0, PH + FHT_WF, 16, w, lane);  // Wf^T for the edge layer
+    }
+    ECO_TS(21 - layer);
+  }
+
+  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
+  glds_wait();
+  __syncthreads();  // Wf^T landed
+  {
+    const size_t ro = (R0 + rr) * 64 + 4 * s4;
+    float4 due[4];
+    const uint32_t h0m = mask16(rmask, SM_H0), em = mask16(rmask, SM_E);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (valid) st4(GR(GR_DU0) + ro + 16 * c, masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, h0m, c));
+      due[c] = masked(f32x4{de[c].x, de[c].y, de[c].z, de[c].w}, em, c);
+      if (valid) st4(GR(GR_DUE) + ro + 16 * c, due[c]);
+    }
+    f32x4 dg[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kx = node_exp<4>(due);
+    if (has_tile) mm_fh(dg, due, exp2i(kx), WB0, lane);
+    unscale(dg, kx + fh_kw(P, 0));
+    float4 g[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      g[c] = valid ? make_float4(dg[c][0] * rnf, dg[c][1] * rnf, dg[c][2] * rnf, dg[c][3] * rnf) : zero4();
+    if (has_tile) tile_planes(PL, TE, w, rw, s4, g, lane);
+  }
+  __syncthreads();
+  ECO_TS(22);
+  // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
+  {
+    float dwacc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dwacc[i] = 0.f;
+    const AggScale sg = agg_scale(TE, ntiles, lane);
+    f32x4 gp[4], gm[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) gp[nt] = gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (has_tile) {
+      agg2<1>(gp, PL, adjw, sg, kc0, kc1, lane);
+      agg2<2>(gm, PL, adjw, sg, kc0, kc1, lane);
+    }
+    float xk0 = 0.f, xk1 = 0.f;
+    if (valid) {
+      xk0 = a.x[(R0 + rw) * 8 + s4];
+      xk1 = a.x[(R0 + rw) * 8 + 4 + s4];
+    }
+    f32x4 zz[4];
+    lin8(zz, P + PK_WX, xk0, xk1, lane);  // Z exactly as the forward computed it
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float dz4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f = 16 * c + 4 * s4 + i;
+        const float z = zz[c][i];
+        const float wa = P[PK_WA + f];
+        const float tp = fmaf(1.f, wa, z) > 0.f ? __builtin_ldexpf(gp[c][i], -sg.c) : 0.f;
+        const float tm = fmaf(-1.f, wa, z) > 0.f ? __builtin_ldexpf(gm[c][i], -sg.c) : 0.f;
+        dz4[i] = valid ? tp + tm : 0.f;
+        dwacc[4 * c + i] += valid ? tp - tm : 0.f;
+      }
+      if (valid) st4(GR(GR_DZ) + (R0 + rw) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
+    }
+    // reduce dw_a over the 16 node lanes sharing s4, then over waves (fixed order)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float v = dwacc[i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      dwacc[i] = v;
+    }
+    __syncthreads();  // every wave is done reading the G planes: the region becomes the dwa scratch
+    float* REDW = lds;  // [NW][64]
+    if (c16 == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        st4(REDW + w * 64 + 16 * c + 4 * s4,
+            make_float4(dwacc[4 * c], dwacc[4 * c + 1], dwacc[4 * c + 2], dwacc[4 * c + 3]));
+    }
+    __syncthreads();
+    if (w == 0) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) sacc += REDW[k * 64 + lane];
+      DWA[(size_t)blk * 64 + lane] = sacc;
+    }
+  }
+  ECO_TS(23);
+}
+
+static int mpnn_backward_dense2_launch(const MpnnArgs& a, hipStream_t st) {
+  const int rows_pad = (a.gpb * a.N + 15) & ~15;
+  const size_t lds = dense2_fwd_lds_bytes(rows_pad, a.gpb);
+  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  (void)hipFuncSetAttribute((const void*)mpnn_backward_dense2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  mpnn_backward_dense2_kernel<<<blocks, 64 * DN_NW, lds, st>>>(a);
+  return check_launch("mpnn_backward_dense2");
+}
+
 }  // namespace eco

@@ -2,7 +2,7 @@
 # GPU box: dense2 (fp16x2) forward -- parity tests, then A/B bench against the bf16x3 kernel.
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_mpnn_gpu.py tests/test_dense_gpu.py tests/test_parity_benched_batches_gpu.py \
-  tests/test_parity_bench_sizes_gpu.py tests/test_dqn_gpu.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_parity_bench_sizes_gpu.py tests/test_dqn_gpu.py tests/test_problems_train_gpu.py tests/test_parallel_gpu.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/d2_tests.log 2>&1
 rc=$?
 grep -E "PASS|FAIL|passed|failed|Error" gpurun_out/d2_tests.log | tail -60
