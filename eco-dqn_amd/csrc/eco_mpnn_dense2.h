@@ -42,10 +42,22 @@ constexpr int D2_WBUF = 2 * FH_HALF;                   // fp16 per weight buffer
 constexpr int D2_WBUF_BYTES = D2_WBUF * 2;
 constexpr int D2_TE_INTS = 32;                         // tile exponents: [0..15] current planes, [16..31] V planes
 constexpr int D2_K_EMPTY = 127;                        // tile exponent of an all-zero tile
-
-inline size_t dense2_fwd_lds_bytes(int rows_pad, int gpb) {
-  return (size_t)D2_PL_BYTES + 3 * D2_WBUF_BYTES + D2_TE_INTS * 4 + (size_t)rows_pad * 8 + (size_t)gpb * 12 + 16;
-}
+constexpr int D2_HS_LD = 68;                           // fp32 row stride of the readout's h3 rows (conflict-free)
+constexpr int D2_PL_U16 = DN_MAX_ROWS * D2_HS_LD * 2;  // plane array: 2 planes (57,344 B) or the h3 rows (60,928 B)
+constexpr int D2_MAX_GPB = 52;                         // graphs per block (N >= 4, <= 208 rows)
+static_assert(2 * D2_PLANE <= D2_PL_U16, "planes fit the plane array");
+// The LDS is declared as separate static arrays (planes, three weight buffers, small tables) rather than one
+// dynamic block: the waitcnt pass then knows that an LDS-DMA into one weight buffer cannot alias the planes or
+// another buffer, and does not make the aggregation's plane reads wait for weight fragments still in flight.
+#define ECO_D2_LDS                                                                   \
+  __shared__ __attribute__((aligned(16))) uint16_t sPL[D2_PL_U16];                  \
+  __shared__ __attribute__((aligned(16))) uint16_t sW0[D2_WBUF];                    \
+  __shared__ __attribute__((aligned(16))) uint16_t sW1[D2_WBUF];                    \
+  __shared__ __attribute__((aligned(16))) uint16_t sW2[D2_WBUF];                    \
+  __shared__ int sTE[D2_TE_INTS];                                                    \
+  __shared__ int2 sRI[DN_MAX_ROWS];                                                  \
+  __shared__ int64_t sGB[D2_MAX_GPB];                                                \
+  __shared__ int sMD[D2_MAX_GPB]
 
 // ---- fp16x2 splitting -------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
@@ -126,6 +138,39 @@ __device__ __forceinline__ void mm_fh(f32x4 (&acc)[4], const float4 (&x)[4], flo
   }
 }
 
+// Workgroup barrier for LDS data only: waits for this wave's LDS operations (lgkmcnt), not for its global loads,
+// stores or LDS-DMA (vmcnt).  __syncthreads() would drain vmcnt whenever an LDS-DMA is pending (the fence covers
+// the DMA's LDS writes), which exposes every weight prefetch and global load in flight at the first barrier; here
+// each barrier that publishes DMA-staged weights is preceded by an explicit glds_wait() instead.  The "memory"
+// clobber keeps the compiler from moving memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// the lane's 8 weights of lin8 (W[16 nt + (l & 15)][l >> 4 | 4 + (l >> 4)], nt = 0..3), loaded ahead of use
+__device__ __forceinline__ void lin8_load(const float* W, int lane, float (&wv)[8]) {
+  const float* wl = W + (lane & 15) * 8 + (lane >> 4);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    wv[2 * nt] = wl[nt * 128];
+    wv[2 * nt + 1] = wl[nt * 128 + 4];
+  }
+}
+// lin8 of eco_mpnn_dense.h on preloaded weights (same products, same order)
+__device__ __forceinline__ void lin8r(f32x4 (&d)[4], const float (&wv)[8], float xk0, float xk1) {
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    d[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[2 * nt], xk0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    d[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[2 * nt + 1], xk1, d[nt], 0, 0, 0);
+  }
+}
+// sum over the 16 lanes of a row (the lanes l with equal l >> 4), every lane of the row gets it
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x128, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x122, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x121, 0xF, 0xF, false));
+  return v;
+}
+
 // node scale of a Linear's inputs (the lane's float4s of every half)
 template <int NC>
 __device__ __forceinline__ int node_exp(const float4 (&x)[NC]) {
@@ -158,22 +203,22 @@ __device__ __forceinline__ int tile_exp(const float4 (&v)[4]) {
   return mx > 0.f ? scale_exp(mx) : D2_K_EMPTY;
 }
 // features 16ft + 4k .. +3 of node j, already scaled, as two fp16 planes
-__device__ __forceinline__ void plane2_store4(uint16_t* PL, int ft, int j, int k, float4 v) {
+__device__ __forceinline__ void plane2_store4(uint16_t* P0, uint16_t* P1, int ft, int j, int k, float4 v) {
   uint32_t h0, l0, h1, l1;
   split2_pk(v.x, v.y, h0, l0);
   split2_pk(v.z, v.w, h1, l1);
   const int o = plane_off(ft, j, k);
-  *reinterpret_cast<uint2*>(PL + o) = make_uint2(h0, h1);
-  *reinterpret_cast<uint2*>(PL + D2_PLANE + o) = make_uint2(l0, l1);
+  *reinterpret_cast<uint2*>(P0 + o) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(P1 + o) = make_uint2(l0, l1);
 }
 // the tile's four float4 (node-operand layout) scaled by 2^k into the planes; lane 0 records k in TE[tile]
-__device__ __forceinline__ void tile_planes(uint16_t* PL, int* TE, int tile, int r, int s4, const float4 (&v)[4],
-                                            int lane) {
+__device__ __forceinline__ void tile_planes(uint16_t* P0, uint16_t* P1, int* TE, int tile, int r, int s4,
+                                            const float4 (&v)[4], int lane) {
   const int k = tile_exp(v);
   const float sf = exp2i(k == D2_K_EMPTY ? 0 : k);
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    plane2_store4(PL, c, r, s4, make_float4(v[c].x * sf, v[c].y * sf, v[c].z * sf, v[c].w * sf));
+    plane2_store4(P0, P1, c, r, s4, make_float4(v[c].x * sf, v[c].y * sf, v[c].z * sf, v[c].w * sf));
   if (lane == 0) TE[tile] = k;
 }
 
@@ -232,8 +277,8 @@ __device__ __forceinline__ f16x8 adj_frag2(uint32_t W, uint32_t PPlo, uint32_t P
 // acc[ft] += sum over chunks kc in [kc0, kc1) and both planes of Hs[j][16ft + ..] . B[j][node] (products h 2^c);
 // adjw[kc]: spread adjacency words; sc: agg_scale of the planes.  EXEC all ones (wave-uniform branches only).
 template <int MODE>
-__device__ __forceinline__ void agg2(f32x4 (&acc)[4], const uint16_t* PL, const uint32_t (&adjw)[DN_KC],
-                                     const AggScale& sc, int kc0, int kc1, int lane) {
+__device__ __forceinline__ void agg2(f32x4 (&acc)[4], const uint16_t* P0, const uint16_t* P1,
+                                     const uint32_t (&adjw)[DN_KC], const AggScale& sc, int kc0, int kc1, int lane) {
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;
@@ -243,12 +288,12 @@ __device__ __forceinline__ void agg2(f32x4 (&acc)[4], const uint16_t* PL, const 
     const uint32_t plo = __builtin_amdgcn_readlane(sc.pat, 2 * kc);
     const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
     const f16x8 bf = adj_frag2<MODE>(adjw[kc], plo, phi);
-    const uint16_t* base = PL + (32 * kc + j_in) * 16 + 4 * pc;
+    const int off = (32 * kc + j_in) * 16 + 4 * pc;
 #pragma unroll
     for (int p = 1; p >= 0; --p) {  // the small plane first
 #pragma unroll
       for (int ft = 0; ft < 4; ++ft) {
-        const uint16_t* a = base + p * D2_PLANE + ft * (DN_KPMAX * 16);
+        const uint16_t* a = (p ? P1 : P0) + off + ft * (DN_KPMAX * 16);
         const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
         const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         const f16x8 af = __builtin_bit_cast(f16x8, raw);
@@ -261,19 +306,57 @@ __device__ __forceinline__ void agg2(f32x4 (&acc)[4], const uint16_t* PL, const 
 
 // zero the plane rows [rows_pad, KP) (read as zeros by the last k-chunk; no tile writes them)
 template <int NT>
-__device__ __forceinline__ void zero_pad_rows2(uint16_t* PL, int rows_pad) {
+__device__ __forceinline__ void zero_pad_rows2(uint16_t* P0, uint16_t* P1, int rows_pad) {
   const int KP = (rows_pad + 31) & ~31;
   for (int i = threadIdx.x; i < (KP - rows_pad) * 2 * 4 * 4; i += NT) {
     const int k = i & 3, ft = (i >> 2) & 3, p = (i >> 4) & 1, j = rows_pad + (i >> 5);
-    *reinterpret_cast<uint2*>(PL + p * D2_PLANE + plane_off(ft, j, k)) = make_uint2(0u, 0u);
+    *reinterpret_cast<uint2*>((p ? P1 : P0) + plane_off(ft, j, k)) = make_uint2(0u, 0u);
   }
 }
 
-// LDS: PL 2 fp16 planes | WB0 | WB1 | WB2 (32 KB each: Linear fragments; WB1..WB2 hold the V planes of the edge
-//      layer, the readout uses PL..WB0 for fp32 h3 rows and WB1 as scratch) | TE [32] | RI [rows_pad] | GB | MD
+
+// Per-lane staging of the block: the row's norm (deg clamped 0 -> 1, mpnn.py:34-38), its graph's max degree and
+// the adjacency operand as spread words.  One graph per block with a prepared gs.adjbits (ER-200 ... ER-224): the
+// lane loads its own degree and bitmask right after the block's graph id (two dependent global round trips, no
+// LDS table and no barrier); otherwise the row-info table, edge bases and max degrees are staged in LDS and the
+// bitmask is built from the CSR rows (dense_adjacency, with its barriers).
+template <int NT>
+__device__ __forceinline__ void d2_stage(const MpnnArgs& a, int blk, int rows_pad, int rows_valid, int r, bool valid,
+                                         int s4, int2* RI, int64_t* GB, int* MD, uint32_t* ADJ, float& nf, int& md,
+                                         uint32_t (&adjw)[DN_KC]) {
+  const int N = a.N;
+  const int rr = min(r, rows_pad - 1);
+  uint32_t adjb[4];
+  if (a.gpb == 1 && a.gs.adjbits != nullptr) {
+    const int gid = a.gids[blk];  // uniform: scalar load
+    const int dg = valid ? a.gs.deg[(size_t)gid * N + r] : 1;
+    md = a.gs.max_deg[gid];
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (valid) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + r) * 4 + s4) * 4);
+    adjb[0] = v.x; adjb[1] = v.y; adjb[2] = v.z; adjb[3] = v.w;
+    nf = (float)max(dg, 1);
+  } else {
+    const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+    for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
+    for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
+      const int gid = a.gids[blk * a.gpb + gl];
+      GB[gl] = a.gs.edge_base[gid];
+      MD[gl] = a.gs.max_deg[gid];
+    }
+    lds_barrier();
+    nf = (float)row_info(RI, rr).norm;
+    md = valid ? MD[r / N] : 1;
+    dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
+  }
+#pragma unroll
+  for (int kc = 0; kc < DN_KC; ++kc) adjw[kc] = adj_spread((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+}
+
+// LDS (ECO_D2_LDS): sPL the 2 fp16 planes (the readout's fp32 h3 rows at the end) | sW0, sW1, sW2 32-KB Linear
+//      fragment buffers (sW1 / sW2 hold the V planes of the edge layer; sW1 is the readout scratch) | TE | RI | GB | MD
 template <bool SAVE>
 __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(MpnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_D2_LDS;
   ECO_TS(0);
   constexpr int NW = DN_NW;
   constexpr int NT = 64 * NW;
@@ -285,16 +368,16 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
   const int rows_valid = g_valid * N;
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
-  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
-  uint16_t* WB0 = PL + 2 * D2_PLANE;
-  uint16_t* WB1 = WB0 + D2_WBUF;
-  uint16_t* WB2 = WB1 + D2_WBUF;
-  uint16_t* VPL = WB1;  // V planes of the edge layer (57,344 B of WB1..WB2)
-  int* TE = reinterpret_cast<int*>(WB2 + D2_WBUF);
-  int2* RI = reinterpret_cast<int2*>(TE + D2_TE_INTS);
-  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
-  int* MD = reinterpret_cast<int*>(GB + a.gpb);
-  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);  // [rows_pad][DN_ADJW] while a bitmask is built
+  uint16_t* PL = sPL;
+  uint16_t* PL1 = sPL + D2_PLANE;
+  uint16_t* WB0 = sW0;
+  uint16_t* WB1 = sW1;
+  uint16_t* WB2 = sW2;
+  int* TE = sTE;
+  int2* RI = sRI;
+  int64_t* GB = sGB;
+  int* MD = sMD;
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(sPL);  // [rows_pad][DN_ADJW] while a bitmask is built
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
   const float* P = a.P;
@@ -305,47 +388,40 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
   const bool has_tile = w < ntiles;
   const int r = w * 16 + c16;
   const bool valid = has_tile && r < rows_valid;
+  // ---- staging: Wf fragments (LDS-DMA); node features, the 8-input Linears' weights and w_a; row norm, max
+  //      degree and adjacency operand of the lane (d2_stage) ----
+  glds_frags<NW>(WB0, PH + FH_WF, 16, w, lane);
   float xk0 = 0.f, xk1 = 0.f;
   if (valid) {
     xk0 = a.x[(R0 + r) * 8 + s4];
     xk1 = a.x[(R0 + r) * 8 + 4 + s4];
   }
-  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree ----
-  glds_frags<NW>(WB0, PH + FH_WF, 16, w, lane);
-  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
-  for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
-    const int gid = a.gids[blk * a.gpb + gl];
-    GB[gl] = a.gs.edge_base[gid];
-    MD[gl] = a.gs.max_deg[gid];
-  }
-  __syncthreads();
+  float wx8[8], w08[8];
+  lin8_load(P + PK_WX, lane, wx8);
+  lin8_load(P + PK_W0, lane, w08);
+  float4 wa4[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
+  float nf;
+  int md_graph;
+  uint32_t adjw[DN_KC];
+  d2_stage<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, RI, GB, MD, ADJ, nf, md_graph, adjw);
   ECO_TS(1);
-  const int rr = min(r, rows_pad - 1);
-  const RowInfo ri = row_info(RI, rr);
-  const float nf = (float)ri.norm;
   const float rnf = 1.f / nf;
   const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
-  uint32_t adjw[DN_KC];
-  {
-    uint32_t adjb[4];
-    dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
-#pragma unroll
-    for (int kc = 0; kc < DN_KC; ++kc) adjw[kc] = adj_spread((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
-  }
-  zero_pad_rows2<NT>(PL, rows_pad);
-  zero_pad_rows2<NT>(VPL, rows_pad);
-  auto wa_of = [&](int c) { return f4(P + PK_WA + 16 * c + 4 * s4); };
+  zero_pad_rows2<NT>(PL, PL1, rows_pad);
+  zero_pad_rows2<NT>(WB1, WB2, rows_pad);  // V planes
 
   // ---- phase A: Z = Wx . x (f32 MFMA); U = relu(Z + w_a) and V = relu(Z - w_a) planes ----
   if (has_tile) {
     f32x4 z[4];
-    lin8(z, P + PK_WX, xk0, xk1, lane);
+    lin8r(z, wx8, xk0, xk1);
     float4 u[4], v[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float4 wa = wa_of(c);
+      const float4 wa = wa4[c];
       u[c] = valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
                                  relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
                    : zero4();
@@ -353,11 +429,11 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
                                  relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
                    : zero4();
     }
-    tile_planes(PL, TE, w, r, s4, u, lane);
-    tile_planes(VPL, TE + 16, w, r, s4, v, lane);
+    tile_planes(PL, PL1, TE, w, r, s4, u, lane);
+    tile_planes(WB1, WB2, TE + 16, w, r, s4, v, lane);
   }
   glds_wait();  // Wf fragments
-  __syncthreads();
+  lds_barrier();
   ECO_TS(2);
 
   // ---- phase B: edge embedding (mpnn.py:89-104): (A+ . relu(Z + w_a) + A- . relu(Z - w_a)) / norm; Wf ----
@@ -369,8 +445,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
 #pragma unroll
     for (int ft = 0; ft < 4; ++ft) ea[ft] = ev[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (has_tile) {
-      agg2<1>(ea, PL, adjw, su, kc0, kc1, lane);
-      agg2<2>(ev, VPL, adjw, sv, kc0, kc1, lane);
+      agg2<1>(ea, PL, PL1, adjw, su, kc0, kc1, lane);
+      agg2<2>(ev, WB1, WB2, adjw, sv, kc0, kc1, lane);
     }
     const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
     float4 acc[4];
@@ -383,7 +459,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
       acc[c] = make_float4(t4[0], t4[1], t4[2], t4[3]);
     }
     // feature 63 = norm / norm.max()  (mpnn.py:102)
-    const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? MD[r / N] : 1);
+    const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? md_graph : 1);
     if (s4 == 3) acc[3].w = nf / (float)md;
     if (!valid) {
 #pragma unroll
@@ -406,7 +482,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
     }
     if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_E, pos_mask(ereg));
   }
-  __syncthreads();  // every wave is done with the U / V planes and with Wf
+  lds_barrier();  // every wave is done with the U / V planes and with Wf
   ECO_TS(3);
   // layer weights: Wm0 -> WB1, Wu0 -> WB2, Wm1 -> WB0 (landed by layer 0's first barrier)
   glds_frags<NW>(WB1, PH + FH_LAYER, 32, w, lane);
@@ -417,16 +493,16 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
   float4 hreg[4];
   {
     f32x4 z[4];
-    lin8(z, P + PK_W0, xk0, xk1, lane);
+    lin8r(z, w08, xk0, xk1);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       hreg[c] = valid ? relu4(z[c]) : zero4();
       if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
     }
-    if (has_tile) tile_planes(PL, TE, w, r, s4, hreg, lane);
+    if (has_tile) tile_planes(PL, PL1, TE, w, r, s4, hreg, lane);
   }
   if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H0, pos_mask(hreg));
-  __syncthreads();
+  lds_barrier();
   ECO_TS(4);
 
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
@@ -447,20 +523,22 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
     f32x4 ag[4];
 #pragma unroll
     for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) agg2<0>(ag, PL, adjw, sh, kc0, kc1, lane);
+    if (has_tile) agg2<0>(ag, PL, PL1, adjw, sh, kc0, kc1, lane);
     float4 agg[4];
     {
       const float sc = __builtin_ldexpf(rnf, -sh.c);
 #pragma unroll
       for (int c = 0; c < 4; ++c) agg[c] = make_float4(ag[c][0] * sc, ag[c][1] * sc, ag[c][2] * sc, ag[c][3] * sc);
     }
-    if (SAVE && valid) {
+    if (layer == 0) ECO_TS(10);
+    glds_wait();
+    lds_barrier();  // B1: planes read by every wave; this layer's weights landed
+    if (layer == 0) ECO_TS(11);
+    if (SAVE && valid) {  // after the wait: stores count in vmcnt with the weight DMA
       float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
 #pragma unroll
       for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
     }
-    glds_wait();
-    __syncthreads();  // B1: planes read by every wave; this layer's weights landed
     // message = relu(Wm . [agg, e])
     float4 mrel[4];
     {
@@ -483,6 +561,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
       for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
       store_mask(a, RT, R0 + r, s4, SM_M0 + layer, pos_mask(mrel));
     }
+    if (layer == 0) ECO_TS(12);
     // h' = relu(Wu . [h, m])
     {
       f32x4 hn[4];
@@ -502,40 +581,114 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
       }
     }
     if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H1 + layer, pos_mask(hreg));
-    if (layer < 2 && has_tile) tile_planes(PL, TE, w, r, s4, hreg, lane);
-    __syncthreads();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
+    if (layer == 0) ECO_TS(13);
+    if (layer < 2 && has_tile) tile_planes(PL, PL1, TE, w, r, s4, hreg, lane);
+    if (layer == 0) ECO_TS(14);
+    lds_barrier();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
     ECO_TS(5 + layer);
   }
 
-  // ---- phase E: readout + act over h3 rows staged as fp32 [rows][LDH] (planes + WB0 region) ----
-  float* Hs = lds;
+  // ---- phase E: readout (mpnn.py:143-159) + act ----
+  if (a.gpb == 1) {
+    // one graph: per node q_local = Wr[64:] . h3 (the lane's 16 features, summed over the node's four lanes) and per
+    // tile the column sums of h3 (DPP sums over the 16 nodes of a lane row) go to LDS from registers; one barrier;
+    // wave 0 reduces the tile partials in tile order, forms p = Wp . mean, relu(p) . Wr[:64], the q values and acts
+    float* COL = reinterpret_cast<float*>(sPL);  // [ntiles][64]
+    float* QL = COL + 16 * 64;                    // [rows_pad] q_local
+    float* MEANS = QL + DN_MAX_ROWS;              // [64]
+    float* QB = MEANS + 64;                       // [rows_pad] q
+    if (has_tile) {
+      float ql = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 wr = f4(P + PK_WR + 64 + 16 * c + 4 * s4);
+        ql = fmaf(hreg[c].x, wr.x, ql);
+        ql = fmaf(hreg[c].y, wr.y, ql);
+        ql = fmaf(hreg[c].z, wr.z, ql);
+        ql = fmaf(hreg[c].w, wr.w, ql);
+      }
+      auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(ql), __float_as_uint(ql), false, false);
+      ql = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+      auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ql), __float_as_uint(ql), false, false);
+      ql = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+      if (s4 == 0) QL[r] = ql;
+      float cs[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        cs[4 * c] = row_sum16(hreg[c].x);
+        cs[4 * c + 1] = row_sum16(hreg[c].y);
+        cs[4 * c + 2] = row_sum16(hreg[c].z);
+        cs[4 * c + 3] = row_sum16(hreg[c].w);
+      }
+      if (c16 == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          st4(COL + w * 64 + 16 * c + 4 * s4, make_float4(cs[4 * c], cs[4 * c + 1], cs[4 * c + 2], cs[4 * c + 3]));
+      }
+    }
+    lds_barrier();
+    if (w == 0) {
+      float cs = 0.f;
+      for (int t = 0; t < ntiles; ++t) cs += COL[t * 64 + lane];  // tile order
+      const float mean = cs / (float)N;
+      MEANS[lane] = mean;
+      wave_lds_sync();
+      const float* wp = P + PK_WP + lane * 64;
+      float p = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float4 wv = f4(wp + 4 * k), mv = f4(MEANS + 4 * k);
+        p = fmaf(wv.x, mv.x, p);
+        p = fmaf(wv.y, mv.y, p);
+        p = fmaf(wv.z, mv.z, p);
+        p = fmaf(wv.w, mv.w, p);
+      }
+      if (SAVE) {
+        a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)blk * 64 + lane] = mean;
+        a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)a.B * 64 + (size_t)blk * 64 + lane] = p;
+      }
+      const float cg = wave_sum_f(relu(p) * P[PK_WR + lane]);
+      const float br = P[PK_BR];
+      for (int i = lane; i < N; i += 64) {
+        const float qv = cg + QL[i] + br;
+        QB[i] = qv;
+        if (a.q) a.q[R0 + i] = qv;
+      }
+      if (a.has_act) {
+        wave_lds_sync();
+        graph_act<NW>(a, QB, blk, 1, R0);
+      }
+    }
+    ECO_TS(8);
+    return;
+  }
+  // several graphs per block: h3 rows staged as fp32 [rows][D2_HS_LD] in the plane array
+  float* Hs = reinterpret_cast<float*>(sPL);
   if (has_tile) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) st4(Hs + r * LDH + 16 * c + 4 * s4, hreg[c]);
+    for (int c = 0; c < 4; ++c) st4(Hs + r * D2_HS_LD + 16 * c + 4 * s4, hreg[c]);
   }
-  __syncthreads();
-  float* Scr = reinterpret_cast<float*>(WB1);
-  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= 2 * D2_WBUF_BYTES;
-  readout_act<SAVE, NW>(a, Hs, LDH, Scr, split, blk, g_valid, rows_valid, R0, RT);
+  lds_barrier();
+  float* Scr = reinterpret_cast<float*>(sW1);
+  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= D2_WBUF_BYTES;
+  if (!split && readout_scratch_floats(rows_pad, a.gpb, NW, false) * 4 > D2_WBUF_BYTES) return;  // launch checks
+  readout_act<SAVE, NW>(a, Hs, D2_HS_LD, Scr, split, blk, g_valid, rows_valid, R0, RT);
   ECO_TS(8);
 }
 
-static int mpnn_forward_dense2_launch(const MpnnArgs& a, bool save, hipStream_t st) {
+static int dense2_check(const MpnnArgs& a) {
   const int rows_pad = (a.gpb * a.N + 15) & ~15;
-  const size_t lds = dense2_fwd_lds_bytes(rows_pad, a.gpb);
-  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
-  if ((size_t)rows_pad * LDH * 4 > (size_t)D2_PL_BYTES + D2_WBUF_BYTES)  // h3 rows must end before WB1
-    return fail(ECO_ERR_ARG, "dense MPNN readout rows exceed the plane + buffer region");
+  if (rows_pad > DN_MAX_ROWS || a.gpb > D2_MAX_GPB) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS tables");
+  if (readout_scratch_floats(rows_pad, a.gpb, DN_NW, false) * 4 > D2_WBUF_BYTES)
+    return fail(ECO_ERR_ARG, "dense MPNN readout scratch exceeds its buffer");
+  return ECO_OK;
+}
+
+static int mpnn_forward_dense2_launch(const MpnnArgs& a, bool save, hipStream_t st) {
+  if (const int rc = dense2_check(a)) return rc;
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  if (save) {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    mpnn_forward_dense2_kernel<true><<<blocks, 64 * DN_NW, lds, st>>>(a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense2_kernel<false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_forward_dense2_kernel<false><<<blocks, 64 * DN_NW, lds, st>>>(a);
-  }
+  if (save) mpnn_forward_dense2_kernel<true><<<blocks, 64 * DN_NW, 0, st>>>(a);
+  else mpnn_forward_dense2_kernel<false><<<blocks, 64 * DN_NW, 0, st>>>(a);
   return check_launch("mpnn_forward_dense2");
 }
 
@@ -571,9 +724,9 @@ __device__ __forceinline__ void mm_fh2(f32x4 (&acc0)[4], f32x4 (&acc1)[4], const
 // gradients and per-graph / per-block partials as mpnn_backward_dense_kernel (the weight-gradient reduction is
 // shared).  A layer's two transposed Linears are resident (three rotating 32-KB buffers: Wu^T, Wm^T, and the next
 // layer's Wu^T prefetched), three barriers per layer (Wm^T landed | G planes ready | planes read).
-// LDS: PL 2 planes (readout scratch first) | WB0 | WB1 | WB2 | TE [16] | RI [rows_pad] int2 | GB [gpb] i64
+// LDS (ECO_D2_LDS): sPL 2 planes (readout scratch first) | sW0, sW1, sW2 | TE | RI | GB
 __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(MpnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  ECO_D2_LDS;
   ECO_TS(16);
   constexpr int NW = DN_NW;
   constexpr int NT = 64 * NW;
@@ -585,14 +738,16 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   const int rows_valid = g_valid * N;
   const int rows_pad = (a.gpb * N + 15) & ~15;
   const int ntiles = rows_pad >> 4;
-  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
-  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);
-  uint16_t* WB0 = PL + 2 * D2_PLANE;
-  uint16_t* WB1 = WB0 + D2_WBUF;
-  uint16_t* WB2 = WB1 + D2_WBUF;
-  int* TE = reinterpret_cast<int*>(WB2 + D2_WBUF);
-  int2* RI = reinterpret_cast<int2*>(TE + D2_TE_INTS);
-  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
+  uint16_t* PL = sPL;
+  uint16_t* PL1 = sPL + D2_PLANE;
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(sPL);
+  float* lds = reinterpret_cast<float*>(sPL);  // readout / dw_a scratch
+  uint16_t* WB0 = sW0;
+  uint16_t* WB1 = sW1;
+  uint16_t* WB2 = sW2;
+  int* TE = sTE;
+  int2* RI = sRI;
+  int64_t* GB = sGB;
   const size_t R0 = (size_t)blk * a.gpb * N;
   const size_t RT = (size_t)a.B * N;
   const float* P = a.P;
@@ -617,25 +772,19 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   glds_frags<NW>(WB0, WUT(2), 32, w, lane);
   glds_frags<NW>(WB1, WMT(2), 32, w, lane);
   glds_frags<NW>(WB2, WUT(1), 32, w, lane);
-  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
-  for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
-  __syncthreads();
   const bool has_tile = w < ntiles;
   const int rw = w * 16 + c16;
   const bool valid = has_tile && rw < rows_valid;
   const int rr = min(rw, rows_pad - 1);
-  const float nf = (float)row_info(RI, rr).norm;
+  float nf;
+  int md_unused;
+  uint32_t adjw[DN_KC];
+  d2_stage<NT>(a, blk, rows_pad, rows_valid, rw, valid, s4, RI, GB, sMD, ADJ, nf, md_unused, adjw);
+  (void)md_unused;
   const float rnf = 1.f / nf;
   const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
-  uint32_t adjw[DN_KC];
-  {
-    uint32_t adjb[4];
-    dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, rw, rr, valid, s4, adjb);
-#pragma unroll
-    for (int kc = 0; kc < DN_KC; ++kc) adjw[kc] = adj_spread((adjb[kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
-  }
   const uint16_t* Msk = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
   const uint4 rmask = valid ? *reinterpret_cast<const uint4*>(Msk + ((R0 + rw) * 4 + s4) * SM_TENSORS)
                             : make_uint4(0u, 0u, 0u, 0u);
@@ -647,7 +796,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   float* RED = DMEAN + a.gpb * 64;       // [gpb][NW][64] (split) or [NW][64]
   const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)D2_PL_BYTES;
   for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
-  __syncthreads();
+  lds_barrier();
   if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
@@ -658,7 +807,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       }
       RED[(gl * NW + w) * 64 + lane] = dwb;
     }
-    __syncthreads();
+    lds_barrier();
   }
   for (int gl = w; gl < g_valid; gl += NW) {
     const int e = blk * a.gpb + gl;
@@ -687,7 +836,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     }
     DWRB[(size_t)e * 64 + lane] = dwb;
   }
-  __syncthreads();
+  lds_barrier();
   // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
   float4 dh[4];
   {
@@ -701,8 +850,9 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
                           fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
     }
   }
-  __syncthreads();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
-  zero_pad_rows2<NT>(PL, rows_pad);
+  glds_wait();     // Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (staged at the start) are read from here on
+  lds_barrier();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
+  zero_pad_rows2<NT>(PL, PL1, rows_pad);
   ECO_TS(18);
 
   // ---- update layers in reverse (mpnn.py:114-120) ----
@@ -719,10 +869,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     {
       const uint32_t hmask = mask16(rmask, SM_H0 + layer + 1);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        dh[c] = masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, hmask, c);
-        if (valid) st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[c]);
-      }
+      for (int c = 0; c < 4; ++c) dh[c] = masked(f32x4{dh[c].x, dh[c].y, dh[c].z, dh[c].w}, hmask, c);
     }
     // [dh_direct, dm] = Wu^T . duu;  dum = dm * [m > 0]
     f32x4 dhd[4];
@@ -738,15 +885,19 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       unscale(dmm, ku);
       const uint32_t mmask = mask16(rmask, SM_M0 + layer);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        dum[c] = masked(dmm[c], mmask, c);
-        if (valid) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
-      }
+      for (int c = 0; c < 4; ++c) dum[c] = masked(dmm[c], mmask, c);
     }
     if (layer == 1) ECO_TS(24);
     glds_wait();
-    __syncthreads();  // B0: Wm^T landed
+    lds_barrier();  // B0: Wm^T landed
     if (layer == 1) ECO_TS(25);
+    if (valid) {  // stored after the wait: stores count in vmcnt with the weight DMA
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[c]);
+        st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[c]);
+      }
+    }
     // [dagg, de] = Wm^T . dum;  G = dagg / norm -> planes
     {
       f32x4 dg[4], dd[4];
@@ -763,10 +914,10 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
         de[c].x += dd[c][0]; de[c].y += dd[c][1]; de[c].z += dd[c][2]; de[c].w += dd[c][3];
         g[c] = valid ? make_float4(dg[c][0] * rnf, dg[c][1] * rnf, dg[c][2] * rnf, dg[c][3] * rnf) : zero4();
       }
-      if (has_tile) tile_planes(PL, TE, w, rw, s4, g, lane);
+      if (has_tile) tile_planes(PL, PL1, TE, w, rw, s4, g, lane);
     }
     if (layer == 1) ECO_TS(26);
-    __syncthreads();  // B1: G planes complete
+    lds_barrier();  // B1: G planes complete
     if (layer == 1) ECO_TS(27);
     // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
     {
@@ -776,7 +927,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       f32x4 ag[4];
 #pragma unroll
       for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (has_tile) agg2<0>(ag, PL, adjw, sg, kc0, kc1, lane);
+      if (has_tile) agg2<0>(ag, PL, PL1, adjw, sg, kc0, kc1, lane);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float t4[4];
@@ -786,7 +937,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       }
     }
     if (layer == 1) ECO_TS(28);
-    __syncthreads();  // B2: planes read; this layer's buffers free
+    lds_barrier();  // B2: planes read; this layer's buffers free
     if (layer == 2) {
       glds_frags<NW>(WB0, WMT(1), 32, w, lane);
       glds_frags<NW>(WB1, WUT(0), 32, w, lane);
@@ -799,7 +950,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
 
   // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
   glds_wait();
-  __syncthreads();  // Wf^T landed
+  lds_barrier();  // Wf^T landed
   {
     const size_t ro = (R0 + rr) * 64 + 4 * s4;
     float4 due[4];
@@ -820,38 +971,43 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       g[c] = valid ? make_float4(dg[c][0] * rnf, dg[c][1] * rnf, dg[c][2] * rnf, dg[c][3] * rnf) : zero4();
-    if (has_tile) tile_planes(PL, TE, w, rw, s4, g, lane);
+    if (has_tile) tile_planes(PL, PL1, TE, w, rw, s4, g, lane);
   }
-  __syncthreads();
+  lds_barrier();
   ECO_TS(22);
   // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
   {
     float dwacc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwacc[i] = 0.f;
+    float xk0 = 0.f, xk1 = 0.f;  // inputs of Z, loaded ahead of the aggregations
+    if (valid) {
+      xk0 = a.x[(R0 + rw) * 8 + s4];
+      xk1 = a.x[(R0 + rw) * 8 + 4 + s4];
+    }
+    float wx8[8];
+    lin8_load(P + PK_WX, lane, wx8);
+    float4 wa4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
     const AggScale sg = agg_scale(TE, ntiles, lane);
     f32x4 gp[4], gm[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) gp[nt] = gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (has_tile) {
-      agg2<1>(gp, PL, adjw, sg, kc0, kc1, lane);
-      agg2<2>(gm, PL, adjw, sg, kc0, kc1, lane);
-    }
-    float xk0 = 0.f, xk1 = 0.f;
-    if (valid) {
-      xk0 = a.x[(R0 + rw) * 8 + s4];
-      xk1 = a.x[(R0 + rw) * 8 + 4 + s4];
+      agg2<1>(gp, PL, PL1, adjw, sg, kc0, kc1, lane);
+      agg2<2>(gm, PL, PL1, adjw, sg, kc0, kc1, lane);
     }
     f32x4 zz[4];
-    lin8(zz, P + PK_WX, xk0, xk1, lane);  // Z exactly as the forward computed it
+    lin8r(zz, wx8, xk0, xk1);  // Z exactly as the forward computed it
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float dz4[4];
+      const float wav[4] = {wa4[c].x, wa4[c].y, wa4[c].z, wa4[c].w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int f = 16 * c + 4 * s4 + i;
         const float z = zz[c][i];
-        const float wa = P[PK_WA + f];
+        const float wa = wav[i];
         const float tp = fmaf(1.f, wa, z) > 0.f ? __builtin_ldexpf(gp[c][i], -sg.c) : 0.f;
         const float tm = fmaf(-1.f, wa, z) > 0.f ? __builtin_ldexpf(gm[c][i], -sg.c) : 0.f;
         dz4[i] = valid ? tp + tm : 0.f;
@@ -861,15 +1017,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     }
     // reduce dw_a over the 16 node lanes sharing s4, then over waves (fixed order)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float v = dwacc[i];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      dwacc[i] = v;
-    }
-    __syncthreads();  // every wave is done reading the G planes: the region becomes the dwa scratch
+    for (int i = 0; i < 16; ++i) dwacc[i] = row_sum16(dwacc[i]);
+    lds_barrier();  // every wave is done reading the G planes: the region becomes the dwa scratch
     float* REDW = lds;  // [NW][64]
     if (c16 == 0) {
 #pragma unroll
@@ -877,7 +1026,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
         st4(REDW + w * 64 + 16 * c + 4 * s4,
             make_float4(dwacc[4 * c], dwacc[4 * c + 1], dwacc[4 * c + 2], dwacc[4 * c + 3]));
     }
-    __syncthreads();
+    lds_barrier();
     if (w == 0) {
       float sacc = 0.f;
 #pragma unroll
@@ -889,13 +1038,9 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
 }
 
 static int mpnn_backward_dense2_launch(const MpnnArgs& a, hipStream_t st) {
-  const int rows_pad = (a.gpb * a.N + 15) & ~15;
-  const size_t lds = dense2_fwd_lds_bytes(rows_pad, a.gpb);
-  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
+  if (const int rc = dense2_check(a)) return rc;
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  (void)hipFuncSetAttribute((const void*)mpnn_backward_dense2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-  mpnn_backward_dense2_kernel<<<blocks, 64 * DN_NW, lds, st>>>(a);
+  mpnn_backward_dense2_kernel<<<blocks, 64 * DN_NW, 0, st>>>(a);
   return check_launch("mpnn_backward_dense2");
 }
 

@@ -199,6 +199,9 @@ __host__ __device__ constexpr int readout_scratch_floats(int rows_pad, int gpb, 
   return (split ? gpb * nw * 64 : 0) + ((gpb + 3) & ~3) + rows_pad;
 }
 
+template <int NW>
+__device__ __forceinline__ void graph_act(const MpnnArgs& a, const float* Qb, int blk, int g_valid, size_t R0);
+
 template <bool SAVE, int NW>
 __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, int ldh, float* Scr, bool split,
                                             int blk, int g_valid, int rows_valid, size_t R0, size_t RT) {
@@ -269,6 +272,16 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
   }
   if (!a.has_act) return;
   __syncthreads();
+  graph_act<NW>(a, Qb, blk, g_valid, R0);
+}
+
+// epsilon-greedy act (dqn.py:453-465, :490-512) of the block's graphs from their q values in LDS (Qb [rows]):
+// wave w handles graphs w, w + NW, ...
+template <int NW>
+__device__ __forceinline__ void graph_act(const MpnnArgs& a, const float* Qb, int blk, int g_valid, size_t R0) {
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int N = a.N;
   for (int gl = w; gl < g_valid; gl += NW) {
     const int e = blk * a.gpb + gl;
     float bestq = -INFINITY;

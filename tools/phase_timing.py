@@ -74,8 +74,12 @@ def main():
     ts = stamps(nblk)
     report(f"forward (no save) B={B} N={N}", ts, list(range(0, 9)), FWD)
     if ts is not None and ts[:, 10].any():
-        report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
-               ["weight staging", "MFMA half 1 issue", "gather", "MFMA half 2", "(drain)", "to barrier"])
+        if os.environ.get("ECO_DENSE_V1"):
+            report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
+                   ["weight staging", "MFMA half 1 issue", "gather", "MFMA half 2", "(drain)", "to barrier"])
+        else:  # mpnn_forward_dense2_kernel
+            report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
+                   ["aggregation", "B1 wait", "message", "update", "h' planes", "B2 wait"])
     q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
     torch.cuda.synchronize()
     report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
@@ -87,9 +91,14 @@ def main():
     ts = stamps(nblk)
     report(f"backward          B={B} N={N}", ts, list(range(16, 24)), BWD)
     if ts is not None and ts[:, 24].any():
-        report("  layer 1 detail (wave 0)", ts, [19, 24, 25, 26, 27, 28, 29, 30, 20],
-               ["h,m loads + duu", "B0 wait", "Wu^T x2 + dum", "B1 wait", "dagg + G planes", "B2 wait",
-                "de + A.G", "B3 wait"])
+        if os.environ.get("ECO_DENSE_V1"):
+            report("  layer 1 detail (wave 0)", ts, [19, 24, 25, 26, 27, 28, 29, 30, 20],
+                   ["h,m loads + duu", "B0 wait", "Wu^T x2 + dum", "B1 wait", "dagg + G planes", "B2 wait",
+                    "de + A.G", "B3 wait"])
+        else:  # mpnn_backward_dense2_kernel
+            report("  layer 1 detail (wave 0)", ts, [19, 24, 25, 26, 27, 28, 20],
+                   ["duu, Wu^T x2, dum", "B0 wait (Wm^T DMA)", "stores, Wm^T x2, G planes", "B1 wait", "A.G",
+                    "B2 wait"])
 
 
 if __name__ == "__main__":
