@@ -393,13 +393,16 @@ def main():
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
                         spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
-    # experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377), batched
+    # experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377), batched, with the large-batch recipe of
+    # tests/test_training_quality_gpu.py: target sync every update_target_frequency / update_frequency gradient
+    # steps and lr 1e-4 x sqrt(M / 64)
+    lr = 1e-4 * (args.minibatch / 64.0) ** 0.5
     agent = DQN(env, lambda: MPNN(device=dev), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
                 replay_start_size=3000, replay_buffer_size=B * 16, gamma=0.95, update_target_frequency=4000,
-                update_learning_rate=False, initial_learning_rate=1e-4, peak_learning_rate=1e-4,
-                final_learning_rate=1e-4, update_frequency=32, minibatch_size=64, train_minibatch=args.minibatch,
+                update_learning_rate=False, initial_learning_rate=lr, peak_learning_rate=lr,
+                final_learning_rate=lr, update_frequency=32, minibatch_size=64, train_minibatch=args.minibatch,
                 initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
-                adam_epsilon=1e-8, seed=seed)
+                adam_epsilon=1e-8, seed=seed, target_sync="grad_steps")
     agent.start()
     train = args.workload == "train"
 
@@ -470,7 +473,9 @@ def main():
                     "(std 0.01)",
             "config": {"workload": wl, "n_spins": n, "envs_per_gpu": B, "max_steps": T,
                        "train_minibatch": args.minibatch, "grad_steps_per_vector_step": agent._k_per_vec if train else 0,
-                       "replay_ratio": 2.0, "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
+                       "replay_ratio": 2.0, "lr": lr, "target_sync": "every %d gradient steps"
+                       % agent.target_sync_grad_steps,
+                       "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,

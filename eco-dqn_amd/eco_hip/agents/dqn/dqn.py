@@ -49,7 +49,7 @@ class DQN:
                  network_save_path='network', evaluate=True, test_envs=None, test_episodes=20,
                  test_frequency=10000, test_save_path='test_scores', test_metric=TestMetric.ENERGY_ERROR,
                  logging=True, seed=None, train_minibatch=None, graph_pool_ids=None, regenerate_graphs=None,
-                 compact_replay=None):
+                 compact_replay=None, target_sync="grad_steps"):
         if isinstance(envs, (list, tuple)):
             if len(envs) != 1:
                 raise NotImplementedError("pass one VecSpinSystem (it already holds B episodes)")
@@ -125,8 +125,15 @@ class DQN:
             self.replay_buffer = ReplayBuffer(replay_buffer_size, self.N, device=self.device, seed=self.seed,
                                               n_obs=envs.n_obs)
         self.replay_ratio = minibatch_size / float(update_frequency)
-        # reference: one target sync per update_target_frequency env-steps = that many
-        # env-steps' worth of replayed samples
+        # reference (dqn.py:332-347): one train_step every update_frequency env-steps and one target sync every
+        # update_target_frequency env-steps, i.e. a sync every update_target_frequency / update_frequency gradient
+        # steps.  target_sync="grad_steps" (default) keeps that count of optimiser steps between syncs whatever
+        # the minibatch ("count sync in gradient steps"); "samples" syncs every
+        # update_target_frequency env-steps' worth of replayed samples instead (the two agree at M = minibatch_size).
+        if target_sync not in ("grad_steps", "samples"):
+            raise ValueError("target_sync must be 'grad_steps' or 'samples'")
+        self.target_sync = target_sync
+        self.target_sync_grad_steps = max(1, int(round(update_target_frequency / float(update_frequency))))
         self.target_sync_samples = update_target_frequency * self.replay_ratio
         self._samples_since_sync = 0.0
         self.graph_pool_ids = (np.arange(self.graphs.n_graphs) if graph_pool_ids is None
@@ -387,7 +394,8 @@ class DQN:
             for _ in range(self._k_per_vec):
                 self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False,
                                                   loss_out=self._loss_slot(self._timestep))
-                if self._samples_since_sync >= self.target_sync_samples:
+                if (self.grad_steps % self.target_sync_grad_steps == 0 if self.target_sync == "grad_steps"
+                        else self._samples_since_sync >= self.target_sync_samples):
                     self.sync_target()
                     self._samples_since_sync = 0.0
         return self._last_loss

@@ -52,11 +52,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--n", type=int, default=200)
-    ap.add_argument("--p", type=float, default=0.15)
+    ap.add_argument("--p", type=float, default=0.15, help="ER p, or BA m with --graph BA")
+    ap.add_argument("--graph", default="ER", choices=["ER", "BA"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, N = args.batch, args.n
-    store = GraphStore.generated("ER", B, N, args.p, seed=1, device=dev)
+    store = GraphStore.generated(args.graph, B, N, args.p if args.graph == "ER" else int(args.p), seed=1, device=dev)
     gids = torch.arange(B, dtype=torch.int32, device=dev)
     g = torch.Generator(device="cpu").manual_seed(0)
     x = torch.zeros(B, N, 8)

@@ -19,7 +19,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def make_agent(B, M, lr, seed, n=20, lr_final=None, target_freq=1000, capacity=None, eps_step=150000):
+def make_agent(B, M, lr, seed, n=20, lr_final=None, target_freq=1000, capacity=None, eps_step=150000,
+               target_sync="grad_steps"):
     from eco_hip.graphs import GraphStore, edge_cap
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
@@ -39,7 +40,8 @@ def make_agent(B, M, lr, seed, n=20, lr_final=None, target_freq=1000, capacity=N
                peak_learning_rate_step=1, final_learning_rate=lr_final if lr_final is not None else lr,
                final_learning_rate_step=10 ** 6, update_frequency=32, minibatch_size=64, train_minibatch=M,
                initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=eps_step,
-               adam_epsilon=1e-8, seed=seed, evaluate=False, test_save_path=None, regenerate_graphs=("ER", 0.15))
+               adam_epsilon=1e-8, seed=seed, evaluate=False, test_save_path=None, regenerate_graphs=("ER", 0.15),
+               target_sync=target_sync)
 
 
 class Evaluator:
@@ -91,9 +93,10 @@ def main():
     ap.add_argument("--eval-every", type=int, default=100000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--target-sync", default="grad_steps", choices=["grad_steps", "samples"])
     a = ap.parse_args()
     agent = make_agent(a.envs, a.minibatch, a.lr, a.seed, lr_final=a.lr_final, target_freq=a.target_freq,
-                       eps_step=a.eps_step)
+                       eps_step=a.eps_step, target_sync=a.target_sync)
     ev = Evaluator()
     ev50 = Evaluator(attempts=50, seed=1)
     curve = [(0, *ev(agent.network))]
@@ -112,6 +115,7 @@ def main():
     torch.cuda.synchronize()
     r50 = ev50(agent.network)
     res = {"envs": a.envs, "minibatch": a.minibatch, "lr": a.lr, "lr_final": a.lr_final, "steps": a.steps,
+           "target_sync": a.target_sync,
            "grad_steps": agent.grad_steps, "wall_s": time.time() - t0, "curve": curve,
            "final_1attempt": curve[-1][1:], "final_50attempts": r50}
     print(json.dumps(res), flush=True)
