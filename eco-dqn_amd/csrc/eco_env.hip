@@ -475,7 +475,7 @@ extern "C" int eco_graphs_prepare(eco_graph_set* gs, eco_stream_t stream) {
 
 extern "C" size_t eco_graphs_adjbits_bytes(int32_t n_spins, int32_t n_graphs) {
   if (n_graphs < 1 || !adjbits_applies(n_spins)) return 0;
-  return (size_t)n_graphs * n_spins * 64;
+  return (size_t)n_graphs * n_spins * adjbits_words_per_node(n_spins) * 4;
 }
 
 extern "C" size_t eco_env_state_bytes(const eco_env_config* cfg, int32_t batch) {

@@ -151,7 +151,9 @@ inline int graphs_per_block(int N, int B) {
 
 // dense-path bitmask adjacency of graphs [first, first + count) into gs->adjbits (eco_mpnn_dense.h)
 int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st);
-inline bool adjbits_applies(int n_spins) { return n_spins > 104 && n_spins <= 224; }
+inline bool adjbits_applies(int n_spins) { return n_spins > 104 && n_spins <= 512; }
+// u32 words of gs->adjbits per node: 4 lane quarters x (4 words up to 224 vertices, 8 above)
+inline int adjbits_words_per_node(int n_spins) { return n_spins <= 224 ? 16 : 32; }
 
 size_t mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch);
 int mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_graph_set* gs, const int32_t* graph_ids,

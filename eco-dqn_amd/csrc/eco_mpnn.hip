@@ -42,6 +42,7 @@ __device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
 }  // namespace eco
 #include "eco_mpnn_dense.h"  // dense-aggregation kernels (after the phase-timing buffer)
 #include "eco_mpnn_dense2.h"  // their fp16x2 successors
+#include "eco_mpnn_dl.h"      // one graph of 224 < N <= 512 per workgroup
 #include "eco_mpnn_shared.h"  // many episodes on one shared large graph (G22)
 namespace eco {
 
@@ -1077,6 +1078,8 @@ extern "C" size_t eco_mpnn_workspace_bytes(int32_t n_spins, int32_t batch) {
     const size_t shared = shared_ws_bytes(n_spins, batch);
     return 256 + (per_ep > shared ? per_ep : shared);
   }
+  if (n_spins > DN_MAX_ROWS)  // + the edge embeddings of the dense kernels for 224 < N <= 512
+    return 256 + (size_t)batch * n_spins * 64 * sizeof(float);
   return 256;  // the call-scope norm.max() slot
 }
 
@@ -1167,6 +1170,9 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
     static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernel
     return v1 ? mpnn_forward_dense_launch(a, saved != nullptr, st) : mpnn_forward_dense2_launch(a, saved != nullptr, st);
   }
+  static const bool no_dl = getenv("ECO_MPNN_NO_DL") != nullptr;  // A/B knob: the CSR-gather kernels
+  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !no_dl && !getenv("ECO_MPNN_NO_DENSE"))
+    return mpnn_forward_dl_launch(a, saved != nullptr, workspace, st);
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
     // one graph shared by every episode (GSet best-cut search): node-major episode-batched kernels
@@ -1226,6 +1232,8 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
     static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernels
     return v1 ? mpnn_backward_dense_launch(a, st) : mpnn_backward_dense2_launch(a, st);
   }
+  static const bool no_dl = getenv("ECO_MPNN_NO_DL") != nullptr;
+  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !no_dl && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dl_launch(a, st);
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");

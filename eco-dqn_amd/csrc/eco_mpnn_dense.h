@@ -301,8 +301,63 @@ __global__ __launch_bounds__(256) void adjbits_kernel(eco_graph_set gs, int firs
   }
 }
 
+// the lane's adjacency bits of k-chunk kc (adj_bits16: nz byte, neg byte, element jj <-> bit jj) spread for the
+// fragment builder: nz of elements 0,2,4,6 -> bits 0..3, neg of them -> 4..7, nz of 1,3,5,7 -> 16..19, neg -> 20..23
+__device__ __forceinline__ uint32_t adj_spread(uint32_t b16) {
+  uint32_t e = b16 & 0x5555u, o = (b16 >> 1) & 0x5555u;
+  e = (e | (e >> 1)) & 0x3333u;
+  e = (e | (e >> 2)) & 0x0F0Fu;
+  o = (o | (o >> 1)) & 0x3333u;
+  o = (o | (o >> 2)) & 0x0F0Fu;
+  return ((e | (e >> 4)) & 0xFFu) | (((o | (o >> 4)) & 0xFFu) << 16);
+}
+// 224 < N <= 512 (eco_mpnn_dl.h): adjbits[g][v][q][DL_AW = 8] -- word m holds chunks 2m (bits 0..15) and 2m + 1
+// (bits 16..31) in the PRE-SPREAD form of adj_spread (its bits 0..7 and 16..23 as one 16-bit value), so the
+// kernels unpack a chunk with one byte permute.  LDS: [N][2 * 16] {nz, neg} words.
+__device__ __forceinline__ uint32_t adj_prespread(uint32_t b16) {
+  const uint32_t s = adj_spread(b16);
+  return (s & 0xFFu) | ((s >> 8) & 0xFF00u);
+}
+__global__ __launch_bounds__(256) void adjbits_dl_kernel(eco_graph_set gs, int first) {
+  extern __shared__ uint32_t bmd[];
+  constexpr int KC = 16, W = 2 * KC;
+  const int g = first + blockIdx.x;
+  const int N = gs.n_spins;
+  for (int i = threadIdx.x; i < N * W; i += 256) bmd[i] = 0u;
+  __syncthreads();
+  const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
+  const uint32_t* ed = gs.edges + gs.edge_base[g];
+  for (int i = threadIdx.x; i < N * 4; i += 256) {
+    const int v = i >> 2;
+    for (int e = rp[v] + (i & 3); e < rp[v + 1]; e += 4) {
+      const uint32_t ex = ed[e];
+      const int j = edge_col(ex);
+      atomicOr(&bmd[v * W + 2 * (j >> 5)], 1u << (j & 31));
+      if (edge_w(ex) < 0) atomicOr(&bmd[v * W + 2 * (j >> 5) + 1], 1u << (j & 31));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N * 4; i += 256) {
+    const int v = i >> 2, q = i & 3;
+    const uint2* row = reinterpret_cast<const uint2*>(bmd + v * W);
+    uint32_t o[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      o[m] = adj_prespread(adj_bits16(row[2 * m], q)) | (adj_prespread(adj_bits16(row[2 * m + 1], q)) << 16);
+    uint4* dst = reinterpret_cast<uint4*>(gs.adjbits + (((size_t)g * N + v) * 4 + q) * 8);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  }
+}
+
 int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st) {
-  adjbits_kernel<<<count, 256, 0, st>>>(*gs, first);
+  if (gs->n_spins <= DN_MAX_ROWS) {
+    adjbits_kernel<<<count, 256, 0, st>>>(*gs, first);
+  } else {
+    const int lds = gs->n_spins * 32 * 4;
+    (void)hipFuncSetAttribute((const void*)adjbits_dl_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    adjbits_dl_kernel<<<count, 256, lds, st>>>(*gs, first);
+  }
   return check_launch("graphs_adjbits");
 }
 

@@ -247,16 +247,6 @@ __device__ __forceinline__ AggScale agg_scale(const int* TE, int ntiles, int lan
   return s;
 }
 
-// the lane's adjacency bits of k-chunk kc (adj_bits16: nz byte, neg byte, element jj <-> bit jj) spread for the
-// fragment builder: nz of elements 0,2,4,6 -> bits 0..3, neg of them -> 4..7, nz of 1,3,5,7 -> 16..19, neg -> 20..23
-__device__ __forceinline__ uint32_t adj_spread(uint32_t b16) {
-  uint32_t e = b16 & 0x5555u, o = (b16 >> 1) & 0x5555u;
-  e = (e | (e >> 1)) & 0x3333u;
-  e = (e | (e >> 2)) & 0x0F0Fu;
-  o = (o | (o >> 1)) & 0x3333u;
-  o = (o | (o >> 2)) & 0x0F0Fu;
-  return ((e | (e >> 4)) & 0xFFu) | (((o | (o >> 4)) & 0xFFu) << 16);
-}
 // B fragment (8 fp16 adjacency entries of the lane's node for the chunk's k slots) from a spread word; PPlo / PPhi:
 // magnitude patterns of the chunk's two tiles.  MODE 0: A (signed); 1: A+ = [A = +1]; 2: A- = [A = -1] as +1.
 template <int MODE>

@@ -196,26 +196,85 @@ __device__ __forceinline__ f32x4 lin8_chunk(const float* W, int c, float xk0, fl
   return __builtin_amdgcn_mfma_f32_16x16x4f32(wl[c * 128 + 4], xk1, d, 0, 0, 0);
 }
 
-// aggregation tile tables: thread (tile t, slot k) -> node perm[16 t + k], its CSR row interleaved with the
-// tile's other rows (padding words 0: column 0, weight 0), and the tile's longest row (slot 0: ranked first)
+// aggregation tile tables: tile t, slot k -> node perm[16 t + k]; the tile's CSR rows interleaved (padding words
+// 0: column 0, weight 0) in a BANK-AWARE order, and the tile's longest row (slot 0: ranked first).
+// In shared_agg_kernel lane 4k + q reads 16 B of row col of slot k's current edge: a ds_read_b128 serves the lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63} (MI355X_MICROARCH.md
+// LDS) = slots {0,3,5,6}, {1,2,4,7}, {8,11,13,14}, {9,10,12,15}, each group four 64-B rows, whose bank quarter is
+// col mod 4.  In CSR order two of the four rows share a quarter at most steps (2.1 LDS cycles per group and
+// step on G22-like ER(2000, 0.01), 48 % of the kernel's LDS cycles measured as bank conflicts).  So one thread
+// per (tile, group) orders its four rows greedily: at every step each slot (fewest residue classes left first)
+// takes its next edge of a quarter no other slot of the group uses at that step -- the class with most edges
+// left -- or, with none free, of the least-used quarter (1.28 cycles per group-step on that graph; no step is
+// added: a row keeps its length).  The neighbour sums change summation order only.
+__device__ __forceinline__ int sh_group_slot(int g, int j) {
+  constexpr uint32_t tab[4] = {0x6530u, 0x7421u, 0xEDB8u, 0xFCA9u};  // slot of position j: nibble j
+  return (tab[g] >> (4 * j)) & 0xF;
+}
 __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
   const int N = a.N;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int t = i >> 4, k = i & 15;
+  const int t = i >> 2, g = i & 3;
   if (t >= sb.nt16) return;
   const int gid = a.gids[0];
   const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
   const uint32_t* eg = a.gs.edges + a.gs.edge_base[gid];
-  const int slot = t * 16 + k;
-  const bool valid = slot < N;
-  const int n = valid ? sb.perm[slot] : 0;
-  const int len = valid ? rp[n + 1] - rp[n] : 0;
   const int n0 = sb.perm[t * 16];
   const int ml = (rp[n0 + 1] - rp[n0] + AG_UNROLL - 1) / AG_UNROLL * AG_UNROLL;
-  sb.tn[slot] = valid ? n : -1;
-  if (k == 0) sb.tml[t] = ml;
+  if (g == 0) sb.tml[t] = ml;
+  int k[4], b[4], len[4], cnt[4][4], cur[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    k[j] = sh_group_slot(g, j);
+    const int slot = t * 16 + k[j];
+    const bool valid = slot < N;
+    const int n = valid ? sb.perm[slot] : 0;
+    b[j] = valid ? rp[n] : 0;
+    len[j] = valid ? rp[n + 1] - rp[n] : 0;
+    sb.tn[slot] = valid ? n : -1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cnt[j][r] = cur[j][r] = 0;
+    for (int e = 0; e < len[j]; ++e) {
+      const int r = edge_col(eg[b[j] + e]) & 3;
+      cnt[j][0] += r == 0; cnt[j][1] += r == 1; cnt[j][2] += r == 2; cnt[j][3] += r == 3;
+    }
+  }
   uint32_t* et = sb.et + (size_t)t * sb.MD * 16;
-  for (int q = 0; q < max(ml, AG_UNROLL); ++q) et[((q >> 2) * 16 + k) * 4 + (q & 3)] = q < len ? eg[rp[n] + q] : 0u;
+  for (int q = 0; q < max(ml, AG_UNROLL); ++q) {
+    int used[4] = {0, 0, 0, 0};
+    int ncls[4], ord[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ncls[j] = (cnt[j][0] > 0) + (cnt[j][1] > 0) + (cnt[j][2] > 0) + (cnt[j][3] > 0);
+      ord[j] = j;
+    }
+#pragma unroll
+    for (int x = 1; x < 4; ++x)  // insertion sort of the four slots by classes left (stable)
+      for (int y = x; y > 0 && ncls[ord[y]] < ncls[ord[y - 1]]; --y) {
+        const int tmp = ord[y]; ord[y] = ord[y - 1]; ord[y - 1] = tmp;
+      }
+    uint32_t word[4] = {0u, 0u, 0u, 0u};
+    for (int x = 0; x < 4; ++x) {
+      const int j = ord[x];
+      if (ncls[j] == 0) continue;
+      int best = -1;
+      for (int r = 0; r < 4; ++r)  // a free quarter with the most edges left
+        if (cnt[j][r] > 0 && used[r] == 0 && (best < 0 || cnt[j][r] > cnt[j][best])) best = r;
+      if (best < 0)
+        for (int r = 0; r < 4; ++r)  // else the least-used quarter (most edges left on ties)
+          if (cnt[j][r] > 0 && (best < 0 || used[r] < used[best] || (used[r] == used[best] && cnt[j][r] > cnt[j][best])))
+            best = r;
+      ++used[best];
+      --cnt[j][best];
+      int e = cur[j][best];
+      uint32_t ex = eg[b[j] + e];
+      while ((edge_col(ex) & 3) != best) ex = eg[b[j] + ++e];
+      cur[j][best] = e + 1;
+      word[j] = ex;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) et[((q >> 2) * 16 + k[j]) * 4 + (q & 3)] = word[j];
+  }
 }
 
 // AG[item] (+)= A^(mode) . src[item] for the items = (slice, chunk, episode) blocks: an item's [N][16] block
@@ -223,10 +282,10 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
 // walk items blockIdx.x, + grid, ...: the NEXT item's block is loaded into registers (8 float4 per thread)
 // while the current one is aggregated, then written to LDS between two barriers.  Lane = (node slot k =
 // lane >> 2 of a 16-node tile, feature quarter q = lane & 3); tiles of 16 nodes ranked by decreasing degree
-// walk their interleaved CSR rows (sb.et) in lockstep, AG_TPW tiles per wave at a time, the next group of
+// walk their interleaved CSR rows (sb.et, bank-aware order) in lockstep, AG_TPW tiles per wave at a time, the next group of
 // AG_UNROLL edge words of each in flight (the loop is bound by the latency of these L2 reads: 16 waves x
 // 2 tiles x 4 words beat 8 waves x 2 x 8 and 8 x 2 x 16, 3.51 / 4.03 / 4.94 ms per configs[4] step);
-// each row is summed in CSR order.
+// each row is summed in the order of sb.et.
 // mode 0: weight w (+-1); +1: edges with w > 0, weight 1; -1: edges with w < 0, weight 1.  accumulate: add
 // to AG (the A- pass of the edge phase).
 // XSRC 0: the block is read from src; 1 / 2 / 3: it is BUILT from the observation rows x (32 B per node) as
@@ -618,7 +677,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   if (a.N > 2048) return fail(ECO_ERR_ARG, "shared-graph MPNN: N > 2048 does not fit one LDS block");
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
-  shared_tiles_kernel<<<(sb.nt16 * 16 + 255) / 256, 256, 0, st>>>(a, sb);
+  shared_tiles_kernel<<<(sb.nt16 * 4 + 255) / 256, 256, 0, st>>>(a, sb);
   const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks
   const int agrid = std::min(items, shared_grid());
   const size_t lds_agg = (size_t)a.N * 64;

@@ -8,7 +8,9 @@ are the oracle tolerances of test_mpnn_gpu / test_dqn_gpu:
   float64 autograd of the oracle.
 Covers one graph per block with the prepared bitmask (N = 150, 200, 224), one graph per block built
 in-kernel (adjbits dropped), several graphs per block (N = 20, 64), padding rows, and the fallback for
-non-unit weights."""
+non-unit weights; and the dense kernels for one graph of 224 < N <= 512 per workgroup (eco_mpnn_dl.h: BA-500,
+N = 512 without padding, 497 with a padded last tile, 300 / 225 with waves of unequal tile counts), whose
+gradients are checked against float64 autograd of the oracle on the GPU."""
 import os
 
 import numpy as np
@@ -119,3 +121,42 @@ def test_non_unit_weights_use_the_csr_path():
     for b in range(B):
         obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), mats[b]])).float()
         assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-5
+
+
+@pytest.mark.parametrize("n,B,kind,param", [(500, 6, "BA", 4), (512, 3, "BA", 4), (497, 3, "BA", 4),
+                                            (300, 5, "ER", 0.05), (225, 4, "ER", 0.15)])
+def test_dense_large_matches_csr_and_oracle(n, B, kind, param):
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ActConfig, ECO_NORM_PER_CALL, ECO_NORM_PER_GRAPH
+    from test_dqn_gpu import _flat_to_dict
+    w, store, x, dq = _inputs(n, B, seed=n + B, kind=kind, param=param)
+    assert store.unit_weights and store.adjbits is not None
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    qd, qsd, gd = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=True)
+    qc, qsc, gc = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=False)
+    assert torch.isfinite(qd).all() and torch.isfinite(gd).all()
+    assert not torch.equal(qd, qc)  # two different kernels ran
+    assert _scaled_err(qd, qc) <= 5e-5 and _scaled_err(qsd, qsc) <= 5e-5
+    wc = {k: v.cuda() for k, v in w.items()}
+    obs = torch.stack([torch.from_numpy(np.vstack([x[b, :, :7].cpu().numpy().T.astype(np.float64), store.dense(b)]))
+                       for b in range(B)]).cuda()
+    with torch.no_grad():
+        for b in range(B):
+            assert _scaled_err(qd[b], mo.forward(wc, obs[b].float()).cpu()) <= 5e-5, b
+    w64 = {k: v.cuda().double().clone().requires_grad_(True) for k, v in w.items()}
+    (mo.forward(w64, obs) * dq.double()).sum().backward()
+    dd, dc = _flat_to_dict(gd), _flat_to_dict(gc)
+    for k in mo.KEYS:
+        ref = w64[k].grad.cpu()
+        err = float((dd[k].double() - ref).norm() / max(float(ref.norm()), 1e-12))
+        assert err < 2e-4, (k, err)
+        err_c = float((dd[k] - dc[k]).norm() / max(float(dc[k].norm()), 1e-12))
+        assert err_c < 2e-2, (k, err_c)
+    # fused greedy act on the dense kernel (per-call norm scope)
+    gids = torch.arange(B, dtype=torch.int32, device="cuda")
+    q = torch.empty(B, n, device="cuda")
+    acts = torch.empty(B, dtype=torch.int32, device="cuda")
+    net.forward_graphs(x, store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=q, act=ActConfig(0.0, 1, 0.0, 7, 0),
+                       actions_out=acts)
+    assert torch.equal(acts.long(), q.argmax(1))

@@ -123,6 +123,52 @@ def test_backward_er200_m2048_matches_autograd():
     assert mean <= max(2e-4, 2 * mean32), (mean, mean32)
 
 
+def test_backward_ba500_m2048_matches_autograd():
+    """configs[3]'s gradient step: BA(500, 4) +-1 graphs at M = 2048 through the dense kernels for one graph of
+    224 < N <= 512 per workgroup (eco_mpnn_dl.h) + the weight-gradient reduction, against float64 autograd of the
+    oracle (chunks of 8 graphs: the oracle's [k, N, N, 63] edge tensor).  Bars as the ER-200 test above."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_CALL
+    n, M, chunk = 500, 2048, 8
+    g = torch.Generator().manual_seed(500)
+    w = mo.init_weights(g, std=0.1)
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    store = GraphStore.random("BA", M, n, 4, seed=78)
+    assert store.unit_weights and store.adjbits is not None
+    x = torch.zeros(M, n, 8)
+    x[:, :, :7] = torch.rand(M, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    dq = torch.randn(M, n, generator=g)
+    xc, dqc = x.cuda(), dq.cuda()
+    gids = torch.arange(M, dtype=torch.int32, device="cuda")
+    saved = torch.empty(MPNN.saved_bytes(n, M), dtype=torch.uint8, device="cuda")
+    q = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL, saved=saved)
+    grad = torch.zeros_like(net.flat)
+    net.backward_graphs(xc, store, gids, saved, dqc, grad)
+    torch.cuda.synchronize()
+    nmax = float(store.max_deg.max())
+    w64 = {k: v.cuda().double().clone().requires_grad_(True) for k, v in w.items()}
+    w32 = {k: v.cuda().clone().requires_grad_(True) for k, v in w.items()}
+    for c0 in range(0, M, chunk):
+        ids = torch.arange(c0, c0 + chunk)
+        obs = _obs(xc[ids], dense_batch(store, ids))
+        q64 = mo.forward(w64, obs.double(), norm_max=nmax)
+        torch.testing.assert_close(q[c0:c0 + chunk].double(), q64.detach(), rtol=1e-4, atol=1e-5)
+        (q64 * dqc[ids].double()).sum().backward()
+        (mo.forward(w32, obs, norm_max=nmax) * dqc[ids]).sum().backward()
+    got = _flat_to_dict(grad)
+    report = {k: (_rel(got[k].double(), w64[k].grad), _rel(w32[k].grad.double(), w64[k].grad)) for k in mo.KEYS}
+    print("BA-500 M=2048 relative L2 error vs float64 autograd (eco-hip, fp32 torch oracle):", report)
+    worst32 = max(e32 for _, e32 in report.values())
+    for k, (err, err32) in report.items():
+        assert err < max(2e-4, 1.5 * worst32), (k, err, err32)
+    mean = np.mean([e for e, _ in report.values()])
+    mean32 = np.mean([e32 for _, e32 in report.values()])
+    assert mean <= max(2e-4, 2 * mean32), (mean, mean32)
+
+
 def test_learn_er200_first_train_step_matches_oracle():
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem

@@ -73,9 +73,15 @@ def main():
         net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL)
     torch.cuda.synchronize()
     ts = stamps(nblk)
-    report(f"forward (no save) B={B} N={N}", ts, list(range(0, 9)), FWD)
+    # dense kernels for 224 < N <= 512 (eco_mpnn_dl.h): stamps 1..4 = staging | edge aggregation | Wf | h0
+    dl = 224 < N <= 512 and args.graph in ("ER", "BA") and not os.environ.get("ECO_MPNN_NO_DL")
+    fwd_names = (["staging", "edge agg (A+, A-)", "Wf", "h0"] + FWD[4:]) if dl else FWD
+    report(f"forward (no save) B={B} N={N}", ts, list(range(0, 9)), fwd_names)
     if ts is not None and ts[:, 10].any():
-        if os.environ.get("ECO_DENSE_V1"):
+        if dl:  # mpnn_forward_dl_kernel
+            report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 5],
+                   ["lo planes + wait", "agg lo", "hi planes + agg hi", "message + update", "B_d wait"])
+        elif os.environ.get("ECO_DENSE_V1"):
             report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
                    ["weight staging", "MFMA half 1 issue", "gather", "MFMA half 2", "(drain)", "to barrier"])
         else:  # mpnn_forward_dense2_kernel
@@ -83,7 +89,7 @@ def main():
                    ["aggregation", "B1 wait", "message", "update", "h' planes", "B2 wait"])
     q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
     torch.cuda.synchronize()
-    report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), FWD)
+    report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), fwd_names)
     dq = torch.zeros_like(q)
     dq[torch.arange(B), torch.randint(0, N, (B,))] = 1e-3
     grad = torch.zeros_like(net.flat)
@@ -92,7 +98,9 @@ def main():
     ts = stamps(nblk)
     report(f"backward          B={B} N={N}", ts, list(range(16, 24)), BWD)
     if ts is not None and ts[:, 24].any():
-        if os.environ.get("ECO_DENSE_V1"):
+        if dl:
+            report("  layer 1 detail (wave 0)", ts, [19, 24, 20], ["Linears + lo planes", "barrier + agg lo/hi"])
+        elif os.environ.get("ECO_DENSE_V1"):
             report("  layer 1 detail (wave 0)", ts, [19, 24, 25, 26, 27, 28, 29, 30, 20],
                    ["h,m loads + duu", "B0 wait", "Wu^T x2 + dum", "B1 wait", "dagg + G planes", "B2 wait",
                     "de + A.G", "B3 wait"])
