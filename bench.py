@@ -94,6 +94,28 @@ def _cpu_model():
         return platform.processor() or platform.machine()
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by this process's cgroup CPU quota (cgroup v2 cpu.max 'quota period', or v1
+    cfs_quota_us / cfs_period_us), rounded up; None when unlimited or unreadable."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max" and int(p) > 0:
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return max(1, math.ceil(q / p)) if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
     """SURVEY.md 8d CPU side-by-side: the reference-cost restatement of env.step (oracle/refcost.py:
     the reference's per-step op mix -- 4 dense J@s matvecs, 2 dense np.outer cuts, the observables
@@ -106,9 +128,14 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
     host cores split evenly over them).  ECO_CPU_BASELINE_PROCS caps the process count (testing)."""
     import subprocess
     try:
-        share = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        share = os.cpu_count() or 1
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    # the CPUs this job may actually use: its affinity set, capped by its cgroup CPU quota (on the GPU box the
+    # affinity set names all 256 host CPUs while the quota grants 16: 256 processes on 16 CPUs measured 0.44x
+    # the rate of 16 processes)
+    share = max(1, min(affinity, quota)) if quota else affinity
     cap = int(os.environ.get("ECO_CPU_BASELINE_PROCS", "0")) or share
     procs = max(1, min(share, cap))
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
@@ -128,7 +155,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
     except (OSError, ValueError, KeyError):
         pass
     return dict(value=float(sum(rates)), unit="env-steps/s", cores=procs, kind="port",
-                nproc=os.cpu_count(), cpu_share=share, cpu_model=_cpu_model(),
+                nproc=os.cpu_count(), cpu_share=share, cpu_affinity=affinity, cgroup_cpu_quota=quota,
+                cpu_model=_cpu_model(),
                 per_core=float(np.mean(rates)), gpus_on_node=gpus_on_node,
                 per_gpu_share=float(sum(rates)) / max(1, gpus_on_node),
                 sample=f"{steps} ER-{n} env.step calls (random actions, T=2N episodes) in {procs} single-threaded "
@@ -137,29 +165,38 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "train", "pmc_hbm.json")
-PMC_SQ = os.path.join(REPO, "profiles", "r02", "train", "pmc_sq_dense.json")
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (~2.5 PF)
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "train", "pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r03", "train", "pmc_sq_dense.json")
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
+# kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
+FWD_NAMES = ("mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
+BWD_NAMES = ("mpnn_backward_dense2_kernel", "mpnn_backward_dense_kernel")
+WGRAD_NAMES = ("wgrad_fh_kernel", "wgrad_bf3_kernel", "wgrad_kernel")
+
+
+def _first(d, names):
+    return next(d[k] for k in names if k in d)
 PMC_GSET = os.path.join(REPO, "profiles", "r02", "gset_pmc", "pmc_hbm.json")
 
 
 def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
-    """MFMA evidence of the dominant kernel from the committed SQ PMC pass (profiles/r02/train/
+    """MFMA evidence of the dominant kernel from the committed SQ PMC pass (profiles/r03/train/
     pmc_sq_dense.json, ER-200 M=2048): MFMA-busy fraction (launch mix of the train loop: inference forwards
-    of act and of s', training forwards with saved activations) and the ratio of ISSUED bf16 MFMA FLOPs
-    (bf16x3 splits, dense N^2 aggregations) to the algorithmic FLOPs, so the issued rate can be priced
-    against the bf16 peak beside the f32-algorithmic fraction."""
+    of act and of s', training forwards with saved activations) and the ratio of ISSUED f16 MFMA FLOPs
+    (fp16x2 splits, dense N^2 aggregations) to the algorithmic FLOPs, so the issued rate can be priced
+    against the f16 peak beside the f32-algorithmic fraction."""
     if (graph, n, M) != ("ER", 200, 2048) or dom != "mpnn_forward_kernel":
         return None
     try:
         with open(PMC_SQ) as f:
             k = json.load(f)["kernels"]
-        inf, trn = k["mpnn_forward_dense_kernel<false>"], k["mpnn_forward_dense_kernel<true>"]
+        inf = _first(k, [n + "<false>" for n in FWD_NAMES])
+        trn = _first(k, [n + "<true>" for n in FWD_NAMES])
     except (OSError, ValueError, KeyError):
         return None
     n_inf, n_trn = 1 + 2 * (B * 2 // M), B * 2 // M  # act + online/target(s') per grad step; online(s) saves
     busy = (n_inf * inf["mfma_busy"] + n_trn * trn["mfma_busy"]) / (n_inf + n_trn)
-    ratio = inf["issued_bf16_flop"] / (flops_per_graph * M)
+    ratio = inf.get("issued_mfma_flop", inf.get("issued_bf16_flop")) / (flops_per_graph * M)
     return {"mfma_busy": busy, "issued_per_algorithmic_flop": ratio, "source": os.path.relpath(PMC_SQ, REPO)}
 
 
@@ -189,12 +226,12 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
     gpb = 1 if n >= 208 else 208 // n
     try:
         if dom == "mpnn_forward_kernel":
-            fw = k["mpnn_forward_dense_kernel"]
+            fw = _first(k, FWD_NAMES)
             act, tr = fw[str((B + gpb - 1) // gpb)], fw[str((M + gpb - 1) // gpb)]
             return (act["hbm_bytes_per_launch"] + 3 * (B * 2 // M) * tr["hbm_bytes_per_launch"]) / \
                 (1 + 3 * (B * 2 // M))
-        bw = k["mpnn_backward_dense_kernel"][str((M + gpb - 1) // gpb)]
-        wg = next(iter(k.get("wgrad_bf3_kernel", k.get("wgrad_kernel")).values()))
+        bw = _first(k, BWD_NAMES)[str((M + gpb - 1) // gpb)]
+        wg = next(iter(_first(k, WGRAD_NAMES).values()))
         return bw["hbm_bytes_per_launch"] + wg["hbm_bytes_per_launch"]
     except (KeyError, StopIteration):
         return None
@@ -467,7 +504,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (MPNN: exact bf16x3-split aggregations + six-product bf16x3 Linears, f32 accumulate; "
+            "dtype": "f32-accurate MPNN on f16 MFMA (fp16x2: every operand a power-of-two-scaled pair of fp16 "
+                     "pieces, 22 significand bits, three products, f32 accumulate; aggregations and Linears alike; "
                      "f32 MFMA on the CSR fallback) / f64+int (env)",
             "data": f"synthetic: seeded {args.graph}({n}, {gparam}) +-1 graphs, one per episode; random-init MPNN "
                     "(std 0.01)",
@@ -479,7 +517,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, profiles/r02/train/pmc_hbm.json)",
+                         "traffic_unit": "HBM bytes per launch (PMC, %s)" % os.path.relpath(PMC_SUMMARY, REPO),
                          "avg_launch_ms": avg_ms, "launches": cnt,
                          "flops_per_launch": fl / max(cnt, 1)},
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
@@ -488,8 +526,8 @@ def main():
         mf = pmc_mfma(dom, B, args.minibatch, n, args.graph, mean_gf) if train else None
         if mf:
             issued = achieved * mf["issued_per_algorithmic_flop"]
-            out["roofline"].update(mfma_busy=mf["mfma_busy"], issued_bf16_tflops=issued,
-                                   bf16_peak=BF16_MFMA_PEAK_TFLOPS, bf16_frac=issued / BF16_MFMA_PEAK_TFLOPS,
+            out["roofline"].update(mfma_busy=mf["mfma_busy"], issued_f16_tflops=issued,
+                                   f16_peak=F16_MFMA_PEAK_TFLOPS, f16_frac=issued / F16_MFMA_PEAK_TFLOPS,
                                    mfma_source=mf["source"])
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline_learn_loop"] = cpu_baseline(n, train=train)

@@ -211,9 +211,18 @@ __device__ __forceinline__ int sh_group_slot(int g, int j) {
   constexpr uint32_t tab[4] = {0x6530u, 0x7421u, 0xEDB8u, 0xFCA9u};  // slot of position j: nibble j
   return (tab[g] >> (4 * j)) & 0xF;
 }
-__global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
+// One thread per (tile, group).  Every per-thread table the greedy indexes with a run-time slot / quarter lives
+// in LDS (in registers such indexing compiles to scratch memory: 310-334 us per call on G22), and each thread
+// first copies its four rows into LDS (the first ST_CAP edges of each, independent loads), so the walk reads LDS;
+// rows longer than ST_CAP (hub vertices) read their tail from global memory.
+constexpr int ST_CAP = 64;
+constexpr int ST_THREADS = 64;
+constexpr int ST_LD = 17;  // ints per thread in the small tables (odd stride: no bank conflicts across threads)
+__global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
+  __shared__ uint32_t rows[ST_THREADS][4][ST_CAP];
+  __shared__ int s_cnt[ST_THREADS * ST_LD], s_cur[ST_THREADS * ST_LD], s_small[ST_THREADS * ST_LD];
   const int N = a.N;
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * ST_THREADS + threadIdx.x;
   const int t = i >> 2, g = i & 3;
   if (t >= sb.nt16) return;
   const int gid = a.gids[0];
@@ -222,55 +231,79 @@ __global__ __launch_bounds__(256) void shared_tiles_kernel(MpnnArgs a, SharedBuf
   const int n0 = sb.perm[t * 16];
   const int ml = (rp[n0 + 1] - rp[n0] + AG_UNROLL - 1) / AG_UNROLL * AG_UNROLL;
   if (g == 0) sb.tml[t] = ml;
-  int k[4], b[4], len[4], cnt[4][4], cur[4][4];
+  uint32_t (*my)[ST_CAP] = rows[threadIdx.x];
+  int* cnt = s_cnt + threadIdx.x * ST_LD;  // [slot j][quarter r] at 4j + r: edges of the quarter left
+  int* cur = s_cur + threadIdx.x * ST_LD;  // [j][r]: next position to scan for quarter r
+  int* bj = s_small + threadIdx.x * ST_LD;  // [0..3] row start, [4..7] ncls, [8..11] ord, [12..15] used
+  int* ncls = bj + 4;
+  int* ord = bj + 8;
+  int* used = bj + 12;
+  int k[4], len[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     k[j] = sh_group_slot(g, j);
     const int slot = t * 16 + k[j];
     const bool valid = slot < N;
     const int n = valid ? sb.perm[slot] : 0;
-    b[j] = valid ? rp[n] : 0;
+    bj[j] = valid ? rp[n] : 0;
     len[j] = valid ? rp[n + 1] - rp[n] : 0;
     sb.tn[slot] = valid ? n : -1;
+  }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cnt[j][r] = cur[j][r] = 0;
+  for (int j = 0; j < 4; ++j) {
+    const int nl = min(len[j], ST_CAP);
+    const int b = bj[j];
+#pragma unroll 8
+    for (int e = 0; e < nl; ++e) my[j][e] = eg[b + e];
+  }
+  auto edge_at = [&](int j, int e) -> uint32_t { return e < ST_CAP ? my[j][e] : eg[bj[j] + e]; };
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
     for (int e = 0; e < len[j]; ++e) {
-      const int r = edge_col(eg[b[j] + e]) & 3;
-      cnt[j][0] += r == 0; cnt[j][1] += r == 1; cnt[j][2] += r == 2; cnt[j][3] += r == 3;
+      const int r = edge_col(edge_at(j, e)) & 3;
+      c0 += r == 0; c1 += r == 1; c2 += r == 2; c3 += r == 3;
     }
+    cnt[4 * j] = c0; cnt[4 * j + 1] = c1; cnt[4 * j + 2] = c2; cnt[4 * j + 3] = c3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cur[4 * j + r] = 0;
   }
   uint32_t* et = sb.et + (size_t)t * sb.MD * 16;
   for (int q = 0; q < max(ml, AG_UNROLL); ++q) {
-    int used[4] = {0, 0, 0, 0};
-    int ncls[4], ord[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ncls[j] = (cnt[j][0] > 0) + (cnt[j][1] > 0) + (cnt[j][2] > 0) + (cnt[j][3] > 0);
+      ncls[j] = (cnt[4 * j] > 0) + (cnt[4 * j + 1] > 0) + (cnt[4 * j + 2] > 0) + (cnt[4 * j + 3] > 0);
       ord[j] = j;
+      used[j] = 0;
     }
-#pragma unroll
     for (int x = 1; x < 4; ++x)  // insertion sort of the four slots by classes left (stable)
       for (int y = x; y > 0 && ncls[ord[y]] < ncls[ord[y - 1]]; --y) {
         const int tmp = ord[y]; ord[y] = ord[y - 1]; ord[y - 1] = tmp;
       }
     uint32_t word[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int j = ord[x];
       if (ncls[j] == 0) continue;
+      const int* cj = cnt + 4 * j;
       int best = -1;
       for (int r = 0; r < 4; ++r)  // a free quarter with the most edges left
-        if (cnt[j][r] > 0 && used[r] == 0 && (best < 0 || cnt[j][r] > cnt[j][best])) best = r;
+        if (cj[r] > 0 && used[r] == 0 && (best < 0 || cj[r] > cj[best])) best = r;
       if (best < 0)
         for (int r = 0; r < 4; ++r)  // else the least-used quarter (most edges left on ties)
-          if (cnt[j][r] > 0 && (best < 0 || used[r] < used[best] || (used[r] == used[best] && cnt[j][r] > cnt[j][best])))
+          if (cj[r] > 0 && (best < 0 || used[r] < used[best] || (used[r] == used[best] && cj[r] > cj[best])))
             best = r;
       ++used[best];
-      --cnt[j][best];
-      int e = cur[j][best];
-      uint32_t ex = eg[b[j] + e];
-      while ((edge_col(ex) & 3) != best) ex = eg[b[j] + ++e];
-      cur[j][best] = e + 1;
-      word[j] = ex;
+      --cnt[4 * j + best];
+      int e = cur[4 * j + best];
+      uint32_t ex = edge_at(j, e);
+      while ((edge_col(ex) & 3) != best) ex = edge_at(j, ++e);
+      cur[4 * j + best] = e + 1;
+      // word of slot j (static register index: j == ord[x] is one of four values)
+      word[0] = j == 0 ? ex : word[0];
+      word[1] = j == 1 ? ex : word[1];
+      word[2] = j == 2 ? ex : word[2];
+      word[3] = j == 3 ? ex : word[3];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) et[((q >> 2) * 16 + k[j]) * 4 + (q & 3)] = word[j];
@@ -677,7 +710,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   if (a.N > 2048) return fail(ECO_ERR_ARG, "shared-graph MPNN: N > 2048 does not fit one LDS block");
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
-  shared_tiles_kernel<<<(sb.nt16 * 4 + 255) / 256, 256, 0, st>>>(a, sb);
+  shared_tiles_kernel<<<(sb.nt16 * 4 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
   const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks
   const int agrid = std::min(items, shared_grid());
   const size_t lds_agg = (size_t)a.N * 64;

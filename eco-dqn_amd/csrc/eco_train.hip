@@ -26,6 +26,12 @@ constexpr int MAX_JOBS = 10;
 #ifndef WGRAD_WG_X
 #define WGRAD_WG_X 3  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
 #endif
+#ifndef WGRAD_FH_WG_X
+#define WGRAD_FH_WG_X 3  // wgrad_fh_kernel: workgroups per CU over all jobs (27 KB LDS each)
+#endif
+#ifndef WGRAD_FH_WAVES
+#define WGRAD_FH_WAVES 3  // wgrad_fh_kernel: register budget for this many waves per SIMD
+#endif
 constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
@@ -275,6 +281,199 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   };
   // loads are issued unconditionally (rows past r1 clamp to r1 - 1 and are masked at the store): a
   // conditional load makes the compiler drain every tile in flight at the join (vmcnt(0))
+  if (r0 < r1) {
+    Regs RA, RB;
+    load_tile(RA, r0);
+    load_tile(RB, r0 + WROWS);
+    for (int rb = r0; rb < r1; rb += 2 * WROWS) {
+      store_tile(RA, rb);
+      __syncthreads();
+      load_tile(RA, rb + 2 * WROWS);
+      compute();
+      __syncthreads();
+      if (rb + WROWS >= r1) break;
+      store_tile(RB, rb + WROWS);
+      __syncthreads();
+      load_tile(RB, rb + 3 * WROWS);
+      compute();
+      __syncthreads();
+    }
+  }
+  float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int t = w + 4 * q;
+    if (t < ntile) {
+      const int it = t >> 1;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
+        slab[o * 128 + 32 * it + jj] = acc[q][k];
+      }
+    }
+  }
+}
+
+// Same reduction on fp16x2 operands (eco_mpnn_dense2.h's numerics) and 32x32x16 f16 MFMAs: the 32-row tiles
+// of dY and X are staged in LDS as f32, transposed to [column][row] (stride 36 floats: the 16 lanes of a
+// ds_read_b128 group hit 16 disjoint 4-bank groups) through the same register double buffers.  Each wave
+// then splits its own operand fragments per 16-row k-step: a power-of-two scale per (16 rows x 32 columns)
+// fragment (its wave-wide max |v| into [2^14, 2^15)), v 2^k = hi + lo in fp16 (22 significand bits), the
+// three products hi.hi + hi.lo + lo.hi into a zeroed f32 accumulator, which is added into the running sum
+// scaled back by 2^-(ka + kb).  Against the bf16x3 kernel: half the MFMAs (3 products instead of 6), two
+// fp16 pieces split from registers after the barrier instead of three bf16 planes before it, 27 KB of LDS
+// instead of 46 KB.  Error per product <= ~2^-21 relative, or 2^-40 of the fragment's largest term.
+constexpr int WF_LD = 36;  // f32 per staged column (32 rows + 4 pad)
+typedef _Float16 wf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 wf16x2 __attribute__((ext_vector_type(2)));
+typedef float wf32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t wf_pk(float a, float b) {
+  const wf32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, wf16x2));
+}
+// eight scaled values -> hi / lo fp16 fragments (v = hi + lo to 2^-22)
+__device__ __forceinline__ void wf_split8(const float4& p, const float4& q, float sf, wf16x8& hi, wf16x8& lo) {
+  const float v[8] = {p.x * sf, p.y * sf, p.z * sf, p.w * sf, q.x * sf, q.y * sf, q.z * sf, q.w * sf};
+  u32x4w h, l;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    h[t] = wf_pk(v[2 * t], v[2 * t + 1]);
+    const wf32x2 back = __builtin_convertvector(__builtin_bit_cast(wf16x2, (uint32_t)h[t]), wf32x2);
+    l[t] = wf_pk(v[2 * t] - back[0], v[2 * t + 1] - back[1]);
+  }
+  hi = __builtin_bit_cast(wf16x8, h);
+  lo = __builtin_bit_cast(wf16x8, l);
+}
+__device__ __forceinline__ float wf_absmax8(const float4& p, const float4& q) {
+  return fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
+               fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+}
+__device__ __forceinline__ float wf_wave_max(float m) {  // non-negative floats order as ints
+  int v = __float_as_int(m);
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false));  // row_ror:8
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xF, 0xF, false));  // row_ror:4
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x122, 0xF, 0xF, false));  // row_ror:2
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x121, 0xF, 0xF, false));  // row_ror:1
+  auto s16 = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = max((int)s16[0], (int)s16[1]);
+  auto s32 = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  return __int_as_float(max((int)s32[0], (int)s32[1]));
+}
+__device__ __forceinline__ int wf_scale_exp(float mx) {  // max 2^k in [2^14, 2^15); 0 for zero / non-finite
+  if (!(mx > 0.f) || mx == INFINITY) return 0;
+  const int k = 15 - __builtin_amdgcn_frexp_expf(mx);
+  return k < -110 ? -110 : (k > 110 ? 110 : k);
+}
+__device__ __forceinline__ float wf_exp2i(int k) {
+  k = k < -126 ? -126 : (k > 127 ? 127 : k);
+  return __int_as_float((k + 127) << 23);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGRAD_FH_WAVES, WGRAD_FH_WAVES))) void wgrad_fh_kernel(WJobs jobs, float* slabs) {
+  constexpr int PY = 64 * WF_LD, PX = 128 * WF_LD;
+  __shared__ __attribute__((aligned(16))) float sY[PY];
+  __shared__ __attribute__((aligned(16))) float sX[PX];
+  int jb = 0;
+  while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
+  const int wg = (int)blockIdx.x - jobs.first[jb], nwg = jobs.nwgj[jb];
+  const WJob& J = jobs.j[jb];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int jj = lane & 31, h = lane >> 5;
+  const int K = J.K1 + J.K2;
+  const int ntile = 2 * ((K + 31) / 32);
+  const int chunk = ((J.R + nwg - 1) / nwg + WROWS - 1) / WROWS * WROWS;
+  const int r0 = wg * chunk;
+  const int r1 = min(J.R, r0 + chunk);
+  const int yc = threadIdx.x & 63, yg = threadIdx.x >> 6;
+  const int xc = threadIdx.x & 127, xg0 = threadIdx.x >> 7;
+  typedef const __attribute__((address_space(1))) float gfloat;
+  const bool xlive = xc < K;
+  gfloat* ysrc = (gfloat*)(J.dY + yc);
+  const float* xsrc = !xlive ? J.X1 : (xc < J.K1 ? J.X1 + xc : J.X2 + (xc - J.K1));
+  int xld = xlive && xc >= J.K1 ? J.ld2 : J.ld1;
+  uint32_t xmask = xlive ? 0xFFFFFFFFu : 0u;
+  asm volatile("" : "+v"(xsrc), "+v"(xld), "+v"(xmask));
+  gfloat* xg = (gfloat*)xsrc;
+  const int rlast = r1 - 1;
+  f32x16 acc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
+  struct Regs {
+    float y[8], x[2][8];
+  };
+  auto load_tile = [&](Regs& R, int rb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + 2 * u) + k, rlast) * (size_t)xld];
+  };
+  auto store8 = [&](float* dst, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  };
+  auto store_tile = [&](Regs& R, int rb) {
+    asm volatile("" : "+s"(rb));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
+    store8(sY + yc * WF_LD + 8 * yg, R.y);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        R.x[u][k] = rb + 8 * (xg0 + 2 * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
+      store8(sX + xc * WF_LD + 8 * (xg0 + 2 * u), R.x[u]);
+    }
+  };
+  const int ot = w & 1;
+  const bool live0 = w < ntile, live1 = w + 4 < ntile;
+  const float* ya = sY + (32 * ot + jj) * WF_LD + 8 * h;
+  const float* xb0 = sX + (32 * (w >> 1) + jj) * WF_LD + 8 * h;
+  const float* xb1 = xb0 + 64 * WF_LD;
+  auto compute = [&]() {
+    if (!live0) return;
+#pragma unroll
+    for (int s = 0; s < WROWS / 16; ++s) {
+      const float4 a0 = *reinterpret_cast<const float4*>(ya + 16 * s);
+      const float4 a1 = *reinterpret_cast<const float4*>(ya + 16 * s + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(xb0 + 16 * s);
+      const float4 b1 = *reinterpret_cast<const float4*>(xb0 + 16 * s + 4);
+      float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
+      if (live1) {
+        c0 = *reinterpret_cast<const float4*>(xb1 + 16 * s);
+        c1 = *reinterpret_cast<const float4*>(xb1 + 16 * s + 4);
+      }
+      const int ka = wf_scale_exp(wf_wave_max(wf_absmax8(a0, a1)));
+      const int kb = wf_scale_exp(wf_wave_max(wf_absmax8(b0, b1)));
+      wf16x8 ah, al, bh, bl;
+      wf_split8(a0, a1, wf_exp2i(ka), ah, al);
+      wf_split8(b0, b1, wf_exp2i(kb), bh, bl);
+      f32x16 t = {};
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, t, 0, 0, 0);
+      const float ub = wf_exp2i(-(ka + kb));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[0][k] = fmaf(t[k], ub, acc[0][k]);
+      if (live1) {
+        const int kc = wf_scale_exp(wf_wave_max(wf_absmax8(c0, c1)));
+        wf16x8 ch, cl;
+        wf_split8(c0, c1, wf_exp2i(kc), ch, cl);
+        f32x16 u = {};
+        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, u, 0, 0, 0);
+        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, u, 0, 0, 0);
+        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, u, 0, 0, 0);
+        const float uc = wf_exp2i(-(ka + kc));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[1][k] = fmaf(u[k], uc, acc[1][k]);
+      }
+    }
+  };
   if (r0 < r1) {
     Regs RA, RB;
     load_tile(RA, r0);
@@ -722,20 +921,34 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
   static const bool f32_wgrad = getenv("ECO_WGRAD_F32") != nullptr;  // A/B switch: the f32-MFMA reduction
+  static const bool fh_wgrad = getenv("ECO_WGRAD_FH") != nullptr;    // A/B switch: the fp16x2 reduction
+  // A/B knob: workgroups of each K = 128 job (Wm, Wu); the other jobs share the rest of the resident wave evenly
+  static const int big_wg = [] { const char* e = getenv("ECO_WGRAD_BIG"); return e ? atoi(e) : 0; }();
   if (f32_wgrad) {
     J.nwg = WG_PER_JOB;
     for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
     wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
   } else {
-    // 46 KB LDS -> 3 workgroups per CU: one resident wave of workgroups over the 256 CUs, split evenly over
-    // the jobs (a split in proportion to the bytes each job reads measured slower: 1.28 vs 1.05 ms per
-    // gradient step of backward + weight gradients at M = 2048 ER-200)
+    // one resident wave of workgroups over the 256 CUs (46 KB LDS: 3 per CU for bf16x3; 27 KB and 168 VGPRs:
+    // 3 per CU for fp16x2), split evenly over the jobs (a split in proportion to the bytes each job reads
+    // measured slower: 1.28 vs 1.05 ms per gradient step of backward + weight gradients at M = 2048 ER-200;
+    // the fp16x2 kernel measured 0.62 vs 0.52 ms per launch: its per-fragment scales and splits sit after the
+    // barrier, on the critical path)
+    const int total = (fh_wgrad ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
+    int nbig = 0;
+    for (int j = 0; j < n; ++j) nbig += J.j[j].K1 + J.j[j].K2 == 128;
     J.first[0] = 0;
     for (int j = 0; j < n; ++j) {
-      J.nwgj[j] = std::min(WG_PER_JOB, WGRAD_WG_X * 256 / n);
+      const bool big = J.j[j].K1 + J.j[j].K2 == 128;
+      int g = total / n;
+      if (big_wg > 0 && nbig > 0 && nbig < n) g = big ? big_wg : (total - nbig * big_wg) / (n - nbig);
+      J.nwgj[j] = std::max(1, std::min(WG_PER_JOB, g));
       J.first[j + 1] = J.first[j] + J.nwgj[j];
     }
-    wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
+    if (fh_wgrad)
+      wgrad_fh_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
+    else
+      wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
   }
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
   colsum_kernel<<<64, 256, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
