@@ -18,25 +18,48 @@ namespace eco {
 
 // ------------------------------------------------------------------ graphs ----
 // score_solver.py:347-375 (normalisers) and mpnn.py:34-38 (degree norm).
-__global__ __launch_bounds__(256) void graphs_prepare_kernel(eco_graph_set gs, int first, int count) {
+// One wave per graph.  The wave streams the graph's edge words ONCE, coalesced (lane l reads edges l, l + 64,
+// ...), and each lane follows its edge's row through the row pointers staged in LDS (rows are contiguous, so a
+// lane's row index only moves forward); per-vertex row sums and nonzero counts are LDS integer atomics (exact,
+// order-free).  Walking one row per lane instead (each lane its own vertex's row) moved 3.58 GB for 8,192
+// ER-200 graphs (18x their CSR): every load instruction touched 64 different lines.
+constexpr int GP_WAVES = 4;
+__global__ __launch_bounds__(64 * GP_WAVES) void graphs_prepare_kernel(eco_graph_set gs, int first, int count) {
+  extern __shared__ int gp_lds[];  // per wave: rp [N + 1], rowsum [N], deg [N]
   const int lane = threadIdx.x & 63;
-  const int g = first + blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= first + count) return;
+  const int wv = threadIdx.x >> 6;
+  const int g = first + blockIdx.x * GP_WAVES + wv;
+  if (g >= first + count) return;  // wave-uniform; no block barrier below
   const int N = gs.n_spins;
+  int* rpl = gp_lds + wv * (3 * N + 1);
+  int* rsum = rpl + N + 1;
+  int* dcnt = rsum + N;
   const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
   const uint32_t* ed = gs.edges + gs.edge_base[g];
-  long long pos = 0, neg = 0, sum = 0;
+  for (int v = lane; v <= N; v += 64) rpl[v] = rp[v];
+  for (int v = lane; v < N; v += 64) rsum[v] = dcnt[v] = 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes done
+  __builtin_amdgcn_wave_barrier();
+  const int e0 = rpl[0], e1 = rpl[N];
+  long long pos = 0, neg = 0;
+  int row = 0;
+  for (int e = e0 + lane; e < e1; e += 64) {
+    while (rpl[row + 1] <= e) ++row;  // the row holding edge e (empty rows skipped)
+    const int w = edge_w(ed[e]);
+    if (w > 0) pos += w; else neg += w;
+    if (w != 0) {
+      atomicAdd(&rsum[row], w);
+      atomicAdd(&dcnt[row], 1);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  long long sum = 0;
   int mdeg = 1;
   int best = INT_MIN;
   int has = 0;
   for (int v = lane; v < N; v += 64) {
-    int rs = 0, d = 0;
-    for (int e = rp[v]; e < rp[v + 1]; ++e) {
-      const int w = edge_w(ed[e]);
-      rs += w;
-      d += (w != 0);
-      if (w > 0) pos += w; else neg += w;
-    }
+    const int rs = rsum[v], d = dcnt[v];
     sum += rs;
     gs.deg[(size_t)g * N + v] = d;
     mdeg = max(mdeg, max(d, 1));
@@ -461,7 +484,9 @@ int eco::graphs_prepare_range(eco_graph_set* gs, int first, int count, hipStream
     return fail(ECO_ERR_ARG, "incomplete graph set");
   if (gs->n_graphs < 1 || gs->n_spins < 1) return fail(ECO_ERR_ARG, "empty graph set");
   if (first < 0 || count < 1 || first + count > gs->n_graphs) return fail(ECO_ERR_ARG, "graph range out of set");
-  graphs_prepare_kernel<<<(count + 3) / 4, 256, 0, st>>>(*gs, first, count);
+  const size_t lds = (size_t)GP_WAVES * (3 * gs->n_spins + 1) * sizeof(int);
+  (void)hipFuncSetAttribute((const void*)graphs_prepare_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  graphs_prepare_kernel<<<(count + GP_WAVES - 1) / GP_WAVES, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
   int rc = check_launch("graphs_prepare");
   if (rc) return rc;
   if (gs->adjbits && gs->unit_weights && adjbits_applies(gs->n_spins)) return adjbits_build(gs, first, count, st);

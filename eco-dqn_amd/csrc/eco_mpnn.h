@@ -127,8 +127,17 @@ enum { GR_DUU0 = 0, GR_DUU1, GR_DUU2, GR_DUM0, GR_DUM1, GR_DUM2, GR_DUE, GR_DU0,
 // uses the same value).  Up to 208 rows per block; within that, the count whose launch is estimated
 // fastest: rounds of blocks over the CUs x (16-row tiles per SIMD + 1 for the block's staging and
 // readout) -- e.g. ER-20 x4096: 8 graphs (10 tiles, 512 blocks) beats 10 (13 tiles, 410 blocks) by 16 %.
-inline int graphs_per_block(int N, int B) {
-  static const int cap = [] { const char* e = getenv("ECO_MPNN_GPB"); return e ? atoi(e) : 0; }();  // A/B knob
+// Forward workspace header (the first 256 B): int 0 = the call's max degree (norm scope per call); bytes
+// [WS_KEY_OFFSET, +16) = the key of the shared-graph tables cached after it (eco_mpnn_shared.h).  Every other
+// path that writes the workspace past the header zeroes the key (ws_invalidate_key), so cached tables it
+// overwrote are rebuilt.
+constexpr int WS_KEY_OFFSET = 64;
+__device__ __forceinline__ void ws_invalidate_key(const int* call_maxdeg) {
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    *reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(const_cast<int*>(call_maxdeg)) + WS_KEY_OFFSET) = 0ull;
+}
+
+inline int device_cu_count() {
   static const int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -136,6 +145,11 @@ inline int graphs_per_block(int N, int B) {
       n = 256;
     return n;
   }();
+  return cus;
+}
+inline int graphs_per_block(int N, int B) {
+  static const int cap = [] { const char* e = getenv("ECO_MPNN_GPB"); return e ? atoi(e) : 0; }();  // A/B knob
+  const int cus = device_cu_count();
   const int gmax = N >= 208 ? 1 : 208 / N;
   if (cap > 0) return cap < gmax ? cap : gmax;
   int best = gmax;

@@ -32,9 +32,17 @@ __device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
   do {                                                                                                      \
     if (threadIdx.x == 0 && blockIdx.x < ECO_TS_BLOCKS) eco_phase_ts[blockIdx.x * 32 + (k)] = wall_clock64(); \
   } while (0)
+// stamps of logical block b (persistent kernels: one workgroup walks several blocks)
+#define ECO_TSB(k, b)                                                                       \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && (b) < ECO_TS_BLOCKS) eco_phase_ts[(b) * 32 + (k)] = wall_clock64(); \
+  } while (0)
 #else
 #define ECO_TS(k) \
   do {            \
+  } while (0)
+#define ECO_TSB(k, b) \
+  do {                \
   } while (0)
 #endif
 
@@ -851,6 +859,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 8 && WLDS ? 2 : 1)) void mpnn_backw
 template <int NW>
 __global__ __launch_bounds__(64 * NW, 2) void mpnn_forward_large_kernel(MpnnArgs a, float* hbuf) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  ws_invalidate_key(a.call_maxdeg);  // hbuf overwrites the cached shared-graph tables
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int e = blockIdx.x;

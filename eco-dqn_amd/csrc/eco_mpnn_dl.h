@@ -168,6 +168,7 @@ template <bool SAVE>
 __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_forward_dl_kernel(MpnnArgs a, float* __restrict__ ebuf) {
   ECO_DL_LDS;
   ECO_TS(0);
+  if (!SAVE) ws_invalidate_key(a.call_maxdeg);  // ebuf (the workspace) overwrites the cached shared-graph tables
   constexpr int NW = DL_NW;
   constexpr int MT = DL_MT;
   constexpr int NT = 64 * NW;

@@ -72,6 +72,7 @@ struct SharedBufs {
   int32_t* tml;   // [nt16] the tile's longest CSR row, rounded up to AG_UNROLL
   uint32_t* et;   // [nt16][MD / 4][16][4] the tile's CSR rows interleaved, four consecutive edges of a slot in one
                   // 16-B word group (edge i of slot k at ((i >> 2) * 16 + k) * 4 + (i & 3); padding: 0)
+  const uint64_t* key;  // workspace header: [0] key of the cached perm / tile tables, [1] 1 = rebuild this call
   int Epad, S, ntiles, nt16, MD;
 };
 
@@ -161,7 +162,45 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
 // perm[rank] = node, nodes ranked by decreasing degree (index on ties).  A workgroup ranks 64 nodes with 4
 // threads per node, each comparing against a quarter of the degrees (staged in LDS in chunks of 2048, read
 // 4 at a time); the four partial counts are summed with shuffles.
+// The degree ranking (perm) and the bank-aware tile tables depend on the graph alone (and on the workspace
+// layout, i.e. N and B), while a G22 best-cut search runs hundreds of forwards on one graph: they are kept in
+// the workspace across calls.  shared_key_kernel hashes (N, B, graph id, the graph's CSR row pointers and edge
+// words) into a 64-bit key (sum of per-word SplitMix64 finalisers: order-aware through the word index) and
+// compares it with the key in the workspace header: equal -> flag 0 (the perm / tiles launches return at once);
+// otherwise the new key is stored and flag 1 rebuilds them in this call (stream order).  A call with another B
+// or N writes its own key into the same header slot, so a layout whose tables it overwrote cannot match later.
+__device__ __forceinline__ uint64_t sh_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void shared_key_kernel(MpnnArgs a, uint64_t* key) {
+  __shared__ uint64_t red[256];
+  const int N = a.N;
+  const int gid = a.gids[0];
+  const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
+  const uint32_t* eg = a.gs.edges + a.gs.edge_base[gid];
+  const int e0 = rp[0], ne = rp[N] - rp[0];
+  uint64_t h = 0;
+  for (int i = threadIdx.x; i <= N; i += 256) h += sh_mix64(((uint64_t)i << 32) ^ (uint32_t)rp[i]);
+  for (int i = threadIdx.x; i < ne; i += 256) h += sh_mix64(((uint64_t)(i + N + 1) << 32) ^ eg[e0 + i]);
+  red[threadIdx.x] = h;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const uint64_t k = red[0] + sh_mix64(((uint64_t)N << 40) ^ ((uint64_t)a.B << 8) ^ 0x5EC0ull) +
+                       sh_mix64(0xC0FFEEull + (uint64_t)gid);
+    const bool same = key[0] == k;
+    key[0] = k;
+    key[1] = same ? 0ull : 1ull;
+  }
+}
+
 __global__ __launch_bounds__(256) void shared_perm_kernel(MpnnArgs a, SharedBufs sb) {
+  if (sb.key[1] == 0ull) return;  // cached from an earlier call on this graph and layout
   __shared__ __attribute__((aligned(16))) int DG[2048];
   const int N = a.N;
   const int i = blockIdx.x * 64 + (threadIdx.x >> 2), part = threadIdx.x & 3;
@@ -219,6 +258,7 @@ constexpr int ST_CAP = 64;
 constexpr int ST_THREADS = 64;
 constexpr int ST_LD = 17;  // ints per thread in the small tables (odd stride: no bank conflicts across threads)
 __global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
+  if (sb.key[1] == 0ull) return;  // cached
   __shared__ uint32_t rows[ST_THREADS][4][ST_CAP];
   __shared__ int s_cnt[ST_THREADS * ST_LD], s_cur[ST_THREADS * ST_LD], s_small[ST_THREADS * ST_LD];
   const int N = a.N;
@@ -709,6 +749,11 @@ __global__ __launch_bounds__(256) void shared_readout_kernel(MpnnArgs a, SharedB
 static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStream_t st) {
   if (a.N > 2048) return fail(ECO_ERR_ARG, "shared-graph MPNN: N > 2048 does not fit one LDS block");
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
+  uint64_t* key = reinterpret_cast<uint64_t*>((char*)workspace + WS_KEY_OFFSET);
+  sb.key = key;
+  static const bool no_cache = getenv("ECO_SHARED_NO_CACHE") != nullptr;  // A/B knob: rebuild every call
+  if (no_cache) (void)hipMemsetAsync(key, 0xFF, 2 * sizeof(uint64_t), st);
+  shared_key_kernel<<<1, 256, 0, st>>>(a, key);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.nt16 * 4 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
   const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks

@@ -924,23 +924,32 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   static const bool fh_wgrad = getenv("ECO_WGRAD_FH") != nullptr;    // A/B switch: the fp16x2 reduction
   // A/B knob: workgroups of each K = 128 job (Wm, Wu); the other jobs share the rest of the resident wave evenly
   static const int big_wg = [] { const char* e = getenv("ECO_WGRAD_BIG"); return e ? atoi(e) : 0; }();
+  static const bool even_wg = getenv("ECO_WGRAD_EVEN") != nullptr;  // A/B knob: the round-2 even split
   if (f32_wgrad) {
     J.nwg = WG_PER_JOB;
     for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
     wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
   } else {
     // one resident wave of workgroups over the 256 CUs (46 KB LDS: 3 per CU for bf16x3; 27 KB and 168 VGPRs:
-    // 3 per CU for fp16x2), split evenly over the jobs (a split in proportion to the bytes each job reads
-    // measured slower: 1.28 vs 1.05 ms per gradient step of backward + weight gradients at M = 2048 ER-200;
-    // the fp16x2 kernel measured 0.62 vs 0.52 ms per launch: its per-fragment scales and splits sit after the
-    // barrier, on the critical path)
+    // 3 per CU for fp16x2).  Measured splits (M = 2048 ER-200): in proportion to the bytes each job reads,
+    // 1.28 vs 1.05 ms per gradient step of backward + weight gradients against an even split; more workgroups
+    // for the K = 128 jobs at the others' expense (ECO_WGRAD_BIG = 96 / 112) slower again (9.25 / 12.1 vs 8.66 ms
+    // per vector step): the K <= 64 jobs cost as much per row.  The fp16x2 kernel measured 0.62 vs 0.52 ms per
+    // launch: its per-fragment scales and splits sit after the barrier, on the critical path.
     const int total = (fh_wgrad ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
     int nbig = 0;
-    for (int j = 0; j < n; ++j) nbig += J.j[j].K1 + J.j[j].K2 == 128;
+    double rows = 0.0;
+    for (int j = 0; j < n; ++j) {
+      nbig += J.j[j].K1 + J.j[j].K2 == 128;
+      rows += J.j[j].R;
+    }
     J.first[0] = 0;
     for (int j = 0; j < n; ++j) {
       const bool big = J.j[j].K1 + J.j[j].K2 == 128;
-      int g = total / n;
+      // in proportion to the job's rows: every job issues the same loads per row (dead X columns read column 0
+      // of the row), so a row costs about the same in every job; the per-graph readout job (R = batch) gets one
+      int g = (int)(total * (double)J.j[j].R / rows);
+      if (even_wg) g = total / n;
       if (big_wg > 0 && nbig > 0 && nbig < n) g = big ? big_wg : (total - nbig * big_wg) / (n - nbig);
       J.nwgj[j] = std::max(1, std::min(WG_PER_JOB, g));
       J.first[j + 1] = J.first[j] + J.nwgj[j];

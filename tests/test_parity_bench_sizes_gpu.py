@@ -347,3 +347,50 @@ def test_shared_graph_forward_hub_and_isolated_nodes():
         with torch.no_grad():
             ref = mo.forward(wc, _obs(xc[b:b + 1], adj))
         assert float(((q1[b] - ref).abs() / (1 + ref.abs())).max()) <= 5e-5, b
+
+
+def test_shared_graph_tables_cache():
+    """The shared-graph path keeps its degree ranking and tile tables in the MPNN workspace across calls, keyed
+    by a hash of the graph and the layout (eco_mpnn_shared.h shared_key_kernel).  A repeated call (tables from
+    the cache) must equal the first bitwise; a call on another graph, a call after the per-episode large kernel
+    overwrote the workspace, and a call after the graph's edge words were changed IN PLACE must each equal a
+    fresh network (own workspace, tables built in that call) bitwise."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_CALL
+    n, B = 600, 8
+    rng = np.random.default_rng(601)
+    J1 = og.er_graph(n, 0.02, rng, weights="discrete")
+    J2 = og.er_graph(n, 0.02, rng, weights="discrete")
+    one1, one2 = GraphStore.from_dense([J1]), GraphStore.from_dense([J2])
+    rep1 = GraphStore.from_dense([J1] * B)
+    g = torch.Generator().manual_seed(61)
+    w = mo.init_weights(g, std=0.1)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    gz = torch.zeros(B, dtype=torch.int32, device="cuda")
+
+    def fresh(store):
+        other = MPNN(device="cuda")
+        other.load_state_dict(w)
+        return other.forward_graphs(xc, store, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    qa = net.forward_graphs(xc, one1, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+    qb = net.forward_graphs(xc, one1, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+    assert torch.equal(qa, qb)
+    qc = net.forward_graphs(xc, one2, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+    assert torch.equal(qc, fresh(one2))
+    net.forward_graphs(xc, rep1, torch.arange(B, dtype=torch.int32, device="cuda"), norm_scope=ECO_NORM_PER_CALL)
+    qd = net.forward_graphs(xc, one1, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+    assert torch.equal(qd, qa)
+    # flip every edge weight in place (+1 <-> -1: still unit weights with both signs, same degrees)
+    e = one1.edges.view(torch.int32)
+    wsign = e >> 24
+    e.copy_((e & 0xFFFFFF) | ((-wsign) << 24))
+    qe = net.forward_graphs(xc, one1, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+    assert not torch.equal(qe, qa)
+    assert torch.equal(qe, fresh(one1))
