@@ -18,53 +18,72 @@ namespace eco {
 
 // ------------------------------------------------------------------ graphs ----
 // score_solver.py:347-375 (normalisers) and mpnn.py:34-38 (degree norm).
-// One wave per graph.  The wave streams the graph's edge words ONCE, coalesced (lane l reads edges l, l + 64,
+// The graph's edge words are streamed ONCE, coalesced (thread t of the graph reads edges t, t + 64 WPG,
 // ...), and each lane follows its edge's row through the row pointers staged in LDS (rows are contiguous, so a
 // lane's row index only moves forward); per-vertex row sums and nonzero counts are LDS integer atomics (exact,
 // order-free).  Walking one row per lane instead (each lane its own vertex's row) moved 3.58 GB for 8,192
 // ER-200 graphs (18x their CSR): every load instruction touched 64 different lines.
 constexpr int GP_WAVES = 4;
+// WPG waves per graph: 1 for N <= 512 (four graphs per workgroup, wave-level sync only), all four for larger
+// graphs (one graph per workgroup: a lone wave took 353 us over the 40 k edge words of a G22-like graph)
+template <int WPG>
 __global__ __launch_bounds__(64 * GP_WAVES) void graphs_prepare_kernel(eco_graph_set gs, int first, int count) {
-  extern __shared__ int gp_lds[];  // per wave: rp [N + 1], rowsum [N], deg [N]
+  extern __shared__ int gp_lds[];  // per graph: rp [N + 1], rowsum [N], deg [N]
+  constexpr int GPB = GP_WAVES / WPG;
+  constexpr int NTG = 64 * WPG;  // threads per graph
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int g = first + blockIdx.x * GP_WAVES + wv;
-  if (g >= first + count) return;  // wave-uniform; no block barrier below
+  const int gl = (int)threadIdx.x / NTG;  // graph of the workgroup
+  const int tg = (int)threadIdx.x % NTG;  // thread within the graph
+  const int g = first + blockIdx.x * GPB + gl;
+  const bool live = g < first + count;  // WPG == 1: wave-uniform; WPG > 1: one graph per workgroup
+  if (WPG == 1 && !live) return;
   const int N = gs.n_spins;
-  int* rpl = gp_lds + wv * (3 * N + 1);
+  int* rpl = gp_lds + gl * (3 * N + 1);
   int* rsum = rpl + N + 1;
   int* dcnt = rsum + N;
+  auto sync = [&]() {
+    if (WPG == 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS operations done
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      __syncthreads();
+    }
+  };
   const int32_t* rp = gs.row_ptr + (size_t)g * (N + 1);
-  const uint32_t* ed = gs.edges + gs.edge_base[g];
-  for (int v = lane; v <= N; v += 64) rpl[v] = rp[v];
-  for (int v = lane; v < N; v += 64) rsum[v] = dcnt[v] = 0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes done
-  __builtin_amdgcn_wave_barrier();
-  const int e0 = rpl[0], e1 = rpl[N];
+  const uint32_t* ed = gs.edges + gs.edge_base[live ? g : first];
+  if (live) {
+    for (int v = tg; v <= N; v += NTG) rpl[v] = rp[v];
+    for (int v = tg; v < N; v += NTG) rsum[v] = dcnt[v] = 0;
+  }
+  sync();
   long long pos = 0, neg = 0;
-  int row = 0;
-  for (int e = e0 + lane; e < e1; e += 64) {
-    while (rpl[row + 1] <= e) ++row;  // the row holding edge e (empty rows skipped)
-    const int w = edge_w(ed[e]);
-    if (w > 0) pos += w; else neg += w;
-    if (w != 0) {
-      atomicAdd(&rsum[row], w);
-      atomicAdd(&dcnt[row], 1);
+  if (live) {
+    const int e0 = rpl[0], e1 = rpl[N];
+    int row = 0;
+    for (int e = e0 + tg; e < e1; e += NTG) {
+      while (rpl[row + 1] <= e) ++row;  // the row holding edge e (empty rows skipped)
+      const int w = edge_w(ed[e]);
+      if (w > 0) pos += w; else neg += w;
+      if (w != 0) {
+        atomicAdd(&rsum[row], w);
+        atomicAdd(&dcnt[row], 1);
+      }
     }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
+  sync();
   long long sum = 0;
   int mdeg = 1;
   int best = INT_MIN;
   int has = 0;
-  for (int v = lane; v < N; v += 64) {
-    const int rs = rsum[v], d = dcnt[v];
-    sum += rs;
-    gs.deg[(size_t)g * N + v] = d;
-    mdeg = max(mdeg, max(d, 1));
-    // g(s=-1)_v = (-1) * (J.(-1))_v = row sum; mlr = max over NONZERO entries
-    if (rs != 0) { has = 1; best = max(best, rs); }
+  if (live) {
+    for (int v = tg; v < N; v += NTG) {
+      const int rs = rsum[v], d = dcnt[v];
+      sum += rs;
+      gs.deg[(size_t)g * N + v] = d;
+      mdeg = max(mdeg, max(d, 1));
+      // g(s=-1)_v = (-1) * (J.(-1))_v = row sum; mlr = max over NONZERO entries
+      if (rs != 0) { has = 1; best = max(best, rs); }
+    }
   }
   pos = wave_sum_ll(pos);
   neg = wave_sum_ll(neg);
@@ -72,6 +91,19 @@ __global__ __launch_bounds__(64 * GP_WAVES) void graphs_prepare_kernel(eco_graph
   mdeg = wave_max_i(mdeg);
   best = wave_max_i(best);
   has = wave_max_i(has);
+  if (WPG > 1) {  // combine the graph's waves (fixed order: integer results, exact anyway)
+    __shared__ long long rpos[GP_WAVES], rneg[GP_WAVES], rsm[GP_WAVES];
+    __shared__ int rmd[GP_WAVES], rbest[GP_WAVES], rhas[GP_WAVES];
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) { rpos[wv] = pos; rneg[wv] = neg; rsm[wv] = sum; rmd[wv] = mdeg; rbest[wv] = best; rhas[wv] = has; }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int k = 1; k < WPG; ++k) {
+      pos += rpos[k]; neg += rneg[k]; sum += rsm[k];
+      mdeg = max(mdeg, rmd[k]); best = max(best, rbest[k]); has = max(has, rhas[k]);
+    }
+    if (!live) return;
+  }
   if (lane == 0) {
     gs.max_deg[g] = mdeg;
     gs.valid[g] = has;
@@ -484,9 +516,17 @@ int eco::graphs_prepare_range(eco_graph_set* gs, int first, int count, hipStream
     return fail(ECO_ERR_ARG, "incomplete graph set");
   if (gs->n_graphs < 1 || gs->n_spins < 1) return fail(ECO_ERR_ARG, "empty graph set");
   if (first < 0 || count < 1 || first + count > gs->n_graphs) return fail(ECO_ERR_ARG, "graph range out of set");
-  const size_t lds = (size_t)GP_WAVES * (3 * gs->n_spins + 1) * sizeof(int);
-  (void)hipFuncSetAttribute((const void*)graphs_prepare_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  graphs_prepare_kernel<<<(count + GP_WAVES - 1) / GP_WAVES, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
+  if (gs->n_spins <= 512) {
+    const size_t lds = (size_t)GP_WAVES * (3 * gs->n_spins + 1) * sizeof(int);
+    (void)hipFuncSetAttribute((const void*)graphs_prepare_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    graphs_prepare_kernel<1><<<(count + GP_WAVES - 1) / GP_WAVES, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
+  } else {
+    const size_t lds = (size_t)(3 * gs->n_spins + 1) * sizeof(int);
+    (void)hipFuncSetAttribute((const void*)graphs_prepare_kernel<GP_WAVES>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    graphs_prepare_kernel<GP_WAVES><<<count, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
+  }
   int rc = check_launch("graphs_prepare");
   if (rc) return rc;
   if (gs->adjbits && gs->unit_weights && adjbits_applies(gs->n_spins)) return adjbits_build(gs, first, count, st);

@@ -713,7 +713,8 @@ __device__ __forceinline__ void mm_fh2(f32x4 (&acc0)[4], f32x4 (&acc1)[4], const
 // products (PK_FH transposed pieces, the matrix scales of the forward).  Writes the same pre-activation
 // gradients and per-graph / per-block partials as mpnn_backward_dense_kernel (the weight-gradient reduction is
 // shared).  A layer's two transposed Linears are resident (three rotating 32-KB buffers: Wu^T, Wm^T, and the next
-// layer's Wu^T prefetched), three barriers per layer (Wm^T landed | G planes ready | planes read).
+// layer's Wu^T prefetched), three barriers per layer (Wm^T landed | G planes ready, the next layers' weights
+// DMA'd | planes read).
 // LDS (ECO_D2_LDS): sPL 2 planes (readout scratch first) | sW0, sW1, sW2 | TE | RI | GB
 __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(MpnnArgs a) {
   ECO_D2_LDS;
@@ -787,7 +788,28 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)D2_PL_BYTES;
   for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
   lds_barrier();
-  if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
+  if (split && a.gpb == 1) {
+    // dWr[64:] = sum_v dq_v h3_v: every wave its own tile's rows (node-operand layout, four float4 per lane),
+    // column sums over the 16 nodes of a lane row (DPP), one [64] partial per wave (zeros without a tile)
+    float4 hv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) hv[c] = valid ? f4(SV(SV_H3) + (R0 + rw) * 64 + 16 * c + 4 * s4) : zero4();
+    const float dqi = valid ? DQ[rw] : 0.f;
+    float cs[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      cs[4 * c] = row_sum16(dqi * hv[c].x);
+      cs[4 * c + 1] = row_sum16(dqi * hv[c].y);
+      cs[4 * c + 2] = row_sum16(dqi * hv[c].z);
+      cs[4 * c + 3] = row_sum16(dqi * hv[c].w);
+    }
+    if (c16 == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        st4(RED + w * 64 + 16 * c + 4 * s4, make_float4(cs[4 * c], cs[4 * c + 1], cs[4 * c + 2], cs[4 * c + 3]));
+    }
+    lds_barrier();
+  } else if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
       float dwb = 0.f;
@@ -811,7 +833,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     if (lane == 0) DBR[e] = S;
     float dmean = 0.f;
 #pragma unroll 16
-    for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
+    for (int k = 0; k < 64; ++k)  // dp_k by readlane (scalar broadcast) instead of a bpermute per k
+      dmean = fmaf(P[PK_WP + k * 64 + lane], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dp), k)), dmean);
     DMEAN[gl * 64 + lane] = dmean / (float)N;
     float dwb = 0.f;
     if (split) {
@@ -907,7 +930,15 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       if (has_tile) tile_planes(PL, PL1, TE, w, rw, s4, g, lane);
     }
     if (layer == 1) ECO_TS(26);
-    lds_barrier();  // B1: G planes complete
+    lds_barrier();  // B1: G planes complete; every wave is past both Linears: this layer's weight buffers free
+    // the next layers' weights go out here rather than after B2: the A^T.G aggregation and B2 hide their DMA
+    if (layer == 2) {
+      glds_frags<NW>(WB0, WMT(1), 32, w, lane);
+      glds_frags<NW>(WB1, WUT(0), 32, w, lane);
+    } else if (layer == 1) {
+      glds_frags<NW>(WB2, WMT(0), 32, w, lane);
+      glds_frags<NW>(WB0, PH + FHT_WF, 16, w, lane);  // Wf^T for the edge layer
+    }
     if (layer == 1) ECO_TS(27);
     // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
     {
@@ -927,14 +958,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
       }
     }
     if (layer == 1) ECO_TS(28);
-    lds_barrier();  // B2: planes read; this layer's buffers free
-    if (layer == 2) {
-      glds_frags<NW>(WB0, WMT(1), 32, w, lane);
-      glds_frags<NW>(WB1, WUT(0), 32, w, lane);
-    } else if (layer == 1) {
-      glds_frags<NW>(WB2, WMT(0), 32, w, lane);
-      glds_frags<NW>(WB0, PH + FHT_WF, 16, w, lane);  // Wf^T for the edge layer
-    }
+    lds_barrier();  // B2: planes read
     ECO_TS(21 - layer);
   }
 

@@ -174,24 +174,25 @@ __device__ __forceinline__ uint64_t sh_mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-__global__ __launch_bounds__(256) void shared_key_kernel(MpnnArgs a, uint64_t* key) {
-  __shared__ uint64_t red[256];
+constexpr int SK_THREADS = 1024;
+__global__ __launch_bounds__(SK_THREADS) void shared_key_kernel(MpnnArgs a, uint64_t* key) {
+  __shared__ uint64_t red[SK_THREADS / 64];
   const int N = a.N;
   const int gid = a.gids[0];
   const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
   const uint32_t* eg = a.gs.edges + a.gs.edge_base[gid];
   const int e0 = rp[0], ne = rp[N] - rp[0];
   uint64_t h = 0;
-  for (int i = threadIdx.x; i <= N; i += 256) h += sh_mix64(((uint64_t)i << 32) ^ (uint32_t)rp[i]);
-  for (int i = threadIdx.x; i < ne; i += 256) h += sh_mix64(((uint64_t)(i + N + 1) << 32) ^ eg[e0 + i]);
-  red[threadIdx.x] = h;
+  for (int i = threadIdx.x; i <= N; i += SK_THREADS) h += sh_mix64(((uint64_t)i << 32) ^ (uint32_t)rp[i]);
+#pragma unroll 4
+  for (int i = threadIdx.x; i < ne; i += SK_THREADS) h += sh_mix64(((uint64_t)(i + N + 1) << 32) ^ eg[e0 + i]);
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);  // sums mod 2^64: any order gives the same key
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    const uint64_t k = red[0] + sh_mix64(((uint64_t)N << 40) ^ ((uint64_t)a.B << 8) ^ 0x5EC0ull) +
+    uint64_t t = 0;
+    for (int k = 0; k < SK_THREADS / 64; ++k) t += red[k];
+    const uint64_t k = t + sh_mix64(((uint64_t)N << 40) ^ ((uint64_t)a.B << 8) ^ 0x5EC0ull) +
                        sh_mix64(0xC0FFEEull + (uint64_t)gid);
     const bool same = key[0] == k;
     key[0] = k;
@@ -753,7 +754,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   sb.key = key;
   static const bool no_cache = getenv("ECO_SHARED_NO_CACHE") != nullptr;  // A/B knob: rebuild every call
   if (no_cache) (void)hipMemsetAsync(key, 0xFF, 2 * sizeof(uint64_t), st);
-  shared_key_kernel<<<1, 256, 0, st>>>(a, key);
+  shared_key_kernel<<<1, SK_THREADS, 0, st>>>(a, key);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.nt16 * 4 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
   const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks
