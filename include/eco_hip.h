@@ -215,7 +215,9 @@ size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch);
  * N > 512 with every graph id naming ONE graph of a single-graph set with +-1 weights (the GSet G22
  * best-cut search of experiments/test_eco.py) takes the shared-graph kernels: the aggregation A.[H_1..H_B]
  * from LDS-staged per-episode blocks, N <= 2048; the workspace (eco_mpnn_workspace_bytes) holds their
- * node-major buffers.
+ * node-major buffers and, across calls, the graph's degree ranking and aggregation tile tables, reused while
+ * a 64-bit key of the graph's CSR, N and the batch matches (rebuilt in the call otherwise; any other path that
+ * writes the workspace invalidates the key), so a caller may pass the same workspace to every call.
  * q[B][N] fp32 (may be NULL when only actions are wanted).
  * act / actions[B]: optional fused epsilon-greedy action selection.
  * saved: NULL for inference; for the training forward of train_step (dqn.py:437)
