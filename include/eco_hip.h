@@ -110,7 +110,8 @@ typedef struct {
                                verify it and report ECO_ERR_GRAPH through eco_check_errors if it is false. */
   uint32_t *adjbits;        /* caller-allocated (eco_graphs_adjbits_bytes) or NULL; filled by eco_graphs_prepare:
                                per graph, node and lane quarter the bitmask adjacency operand of the dense MPNN
-                               kernels ([G][N][4][4] u32), so they skip the per-call CSR -> bitmask build */
+                               kernels ([G][N][4][4] u32 up to N = 224, [G][N][4][8] above, to N = 512), so
+                               they skip the per-call CSR -> bitmask build */
 } eco_graph_set;
 
 /* Graph metadata: MaximumCutUnbiasedScorer normalisers (score_solver.py:347-375)
