@@ -172,12 +172,12 @@ __device__ __forceinline__ void split8_store(uint16_t* base, int plane_stride, c
   *reinterpret_cast<u32x4w*>(base + 2 * plane_stride) = p3;
 }
 
-__global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs) {
+// WIDE: X of up to 128 columns (two 64-column groups per thread); narrow jobs (K <= 64: Wf, W0, Wx, Wp) stage one
+// group of 8 rows x 1 column per thread and issue half the X loads.
+template <bool WIDE>
+__device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, int jb, uint16_t* sY, uint16_t* sX) {
   constexpr int PY = 64 * WB_LD, PX = 128 * WB_LD;  // plane strides (bf16)
-  __shared__ __attribute__((aligned(16))) uint16_t sY[3 * PY];
-  __shared__ __attribute__((aligned(16))) uint16_t sX[3 * PX];
-  int jb = 0;
-  while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
+  constexpr int XU = WIDE ? 2 : 1;                  // X row groups per thread
   const int wg = (int)blockIdx.x - jobs.first[jb], nwg = jobs.nwgj[jb];
   const WJob& J = jobs.j[jb];
   const int lane = threadIdx.x & 63;
@@ -190,7 +190,9 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   const int r1 = min(J.R, r0 + chunk);
   // staging roles: dY column yc of rows 8 yg .. +7; X columns xc (+ 0 / 1 x 128 units) of rows 8 xg .. +7
   const int yc = threadIdx.x & 63, yg = threadIdx.x >> 6;
-  const int xc = threadIdx.x & 127, xg0 = threadIdx.x >> 7;  // units u = t + 256 k: column u & 127, group u >> 7
+  // X: WIDE: column t & 127 of row groups (t >> 7) + 2u, u < 2; narrow: column t & 63 of row group t >> 6
+  const int xc = WIDE ? threadIdx.x & 127 : threadIdx.x & 63, xg0 = WIDE ? threadIdx.x >> 7 : threadIdx.x >> 6;
+  constexpr int XG = WIDE ? 2 : 4;  // row-group step between a thread's X units
   typedef const __attribute__((address_space(1))) float gfloat;
   // loads are unconditional (rows clamped to r1 - 1, dead columns read column 0) and masked after:
   // predicated loads compiled to one branch + vmcnt(0) wait per row, serialising the whole tile
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   // two register buffers: tiles i+1 and i+2 are in flight while tile i is split and multiplied
   // (one tile in flight held the reduction at ~4 TB/s: too few bytes outstanding per CU)
   struct Regs {
-    float y[8], x[2][8];
+    float y[8], x[XU][8];
   };
   // raw loads only; the row / column masks are applied when the tile is stored (masking at load
   // time makes the compiler wait for every load before the multiply it should overlap)
@@ -219,9 +221,9 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
 #pragma unroll
     for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < XU; ++u)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + 2 * u) + k, rlast) * (size_t)xld];
+      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld];
   };
   auto store_tile = [&](Regs& R, int rb) {
     asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
@@ -229,11 +231,11 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
     for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
     split8_store(sY + yc * WB_LD + 8 * yg, PY, R.y);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < XU; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        R.x[u][k] = rb + 8 * (xg0 + 2 * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
-      split8_store(sX + xc * WB_LD + 8 * (xg0 + 2 * u), PX, R.x[u]);
+        R.x[u][k] = rb + 8 * (xg0 + XG * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
+      split8_store(sX + xc * WB_LD + 8 * (xg0 + XG * u), PX, R.x[u]);
     }
   };
   // this wave's output tiles: t = w + 4q -> o-tile w & 1, i-tiles (w >> 1) and (w >> 1) + 2
@@ -312,6 +314,15 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs) {
+  __shared__ __attribute__((aligned(16))) uint16_t sY[3 * 64 * WB_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sX[3 * 128 * WB_LD];
+  int jb = 0;
+  while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
+  if (jobs.j[jb].K1 + jobs.j[jb].K2 > 64) wgrad_bf3_job<true>(jobs, slabs, jb, sY, sX);
+  else wgrad_bf3_job<false>(jobs, slabs, jb, sY, sX);
 }
 
 // Same reduction on fp16x2 operands (eco_mpnn_dense2.h's numerics) and 32x32x16 f16 MFMAs: the 32-row tiles
