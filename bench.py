@@ -165,8 +165,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "train", "pmc_hbm.json")
-PMC_SQ = os.path.join(REPO, "profiles", "r03", "train", "pmc_sq_dense.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "final", "train_pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r03", "final", "pmc_sq_dense.json")
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
 # kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
 FWD_NAMES = ("mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")

@@ -788,28 +788,7 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)D2_PL_BYTES;
   for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
   lds_barrier();
-  if (split && a.gpb == 1) {
-    // dWr[64:] = sum_v dq_v h3_v: every wave its own tile's rows (node-operand layout, four float4 per lane),
-    // column sums over the 16 nodes of a lane row (DPP), one [64] partial per wave (zeros without a tile)
-    float4 hv[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) hv[c] = valid ? f4(SV(SV_H3) + (R0 + rw) * 64 + 16 * c + 4 * s4) : zero4();
-    const float dqi = valid ? DQ[rw] : 0.f;
-    float cs[16];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      cs[4 * c] = row_sum16(dqi * hv[c].x);
-      cs[4 * c + 1] = row_sum16(dqi * hv[c].y);
-      cs[4 * c + 2] = row_sum16(dqi * hv[c].z);
-      cs[4 * c + 3] = row_sum16(dqi * hv[c].w);
-    }
-    if (c16 == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        st4(RED + w * 64 + 16 * c + 4 * s4, make_float4(cs[4 * c], cs[4 * c + 1], cs[4 * c + 2], cs[4 * c + 3]));
-    }
-    lds_barrier();
-  } else if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
+  if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves (dq of a train step: one node per graph)
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
       float dwb = 0.f;

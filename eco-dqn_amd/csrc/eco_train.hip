@@ -540,21 +540,33 @@ __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad)
   grad[J.out_off + o * J.out_ld + J.out_col0 + i] = acc;
 }
 
-// column sums in a fixed order: out[c * out_stride] = sum_r X[r][c]; one workgroup per column,
-// 256 strided partial sums combined by a fixed tree (bitwise reproducible)
-__global__ void colsum_kernel(const float* X, int R, int ld, int C, float* out, int out_stride) {
+// the readout / edge-weight column sums of one backward in ONE launch: one workgroup per output column, blocks
+// dealt to the four jobs in order; a fixed-order sum per column (256 strided partials, then a tree)
+struct ColJob {
+  const float* X;
+  int R, ld, C;
+  float* out;
+  int out_stride;
+};
+struct ColJobs {
+  ColJob j[4];
+  int first[5];
+};
+__global__ void colsum_jobs_kernel(ColJobs jobs) {
+  int jb = 0;
+  while (jb < 3 && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
+  const ColJob& J = jobs.j[jb];
   __shared__ float red[256];
-  const int c = blockIdx.x;
-  if (c >= C) return;
+  const int c = (int)blockIdx.x - jobs.first[jb];
   float acc = 0.f;
-  for (int r = threadIdx.x; r < R; r += 256) acc += X[(size_t)r * ld + c];
+  for (int r = threadIdx.x; r < J.R; r += 256) acc += J.X[(size_t)r * J.ld + c];
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int s2 = 128; s2 > 0; s2 >>= 1) {
     if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[(size_t)c * out_stride] = red[0];
+  if (threadIdx.x == 0) J.out[(size_t)c * J.out_stride] = red[0];
 }
 
 // ---------------------------------------------------------------------- TD ----
@@ -971,10 +983,14 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
       wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
   }
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
-  colsum_kernel<<<64, 256, 0, st>>>(DWRA, batch, 64, 64, grad + fo.Wr, 1);
-  colsum_kernel<<<64, 256, 0, st>>>(DWRB, batch, 64, 64, grad + fo.Wr + 64, 1);
-  colsum_kernel<<<1, 256, 0, st>>>(DBR, batch, 1, 1, grad + fo.Br, 1);
-  colsum_kernel<<<63, 256, 0, st>>>(DWA, nblk, 64, 63, grad + fo.We, 1 + n_obs_in);
+  ColJobs CJ{};
+  CJ.j[0] = ColJob{DWRA, batch, 64, 64, grad + fo.Wr, 1};
+  CJ.j[1] = ColJob{DWRB, batch, 64, 64, grad + fo.Wr + 64, 1};
+  CJ.j[2] = ColJob{DBR, batch, 1, 1, grad + fo.Br, 1};
+  CJ.j[3] = ColJob{DWA, nblk, 64, 63, grad + fo.We, 1 + n_obs_in};
+  CJ.first[0] = 0;
+  for (int k = 0; k < 4; ++k) CJ.first[k + 1] = CJ.first[k] + CJ.j[k].C;
+  colsum_jobs_kernel<<<CJ.first[4], 256, 0, st>>>(CJ);
   return check_launch("mpnn_backward_wgrad");
 }
 

@@ -394,3 +394,29 @@ def test_shared_graph_tables_cache():
     qe = net.forward_graphs(xc, one1, gz, norm_scope=ECO_NORM_PER_CALL).clone()
     assert not torch.equal(qe, qa)
     assert torch.equal(qe, fresh(one1))
+
+
+def test_shared_graph_tables_cache_across_batch_sizes():
+    """The cached tables live at batch-dependent offsets of the workspace: calls on one graph alternating between
+    two batch sizes (the key includes B) must each equal a fresh network's result bitwise."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_CALL
+    n = 600
+    rng = np.random.default_rng(602)
+    J = og.er_graph(n, 0.02, rng, weights="discrete")
+    one = GraphStore.from_dense([J])
+    g = torch.Generator().manual_seed(62)
+    w = mo.init_weights(g, std=0.1)
+    x = torch.zeros(12, n, 8)
+    x[:, :, :7] = torch.rand(12, n, 7, generator=g) * 2 - 1
+    xc = x.cuda()
+    net = MPNN(device="cuda")
+    net.load_state_dict(w)
+    for B in (12, 5, 12, 5):
+        gz = torch.zeros(B, dtype=torch.int32, device="cuda")
+        q = net.forward_graphs(xc[:B].contiguous(), one, gz, norm_scope=ECO_NORM_PER_CALL).clone()
+        other = MPNN(device="cuda")
+        other.load_state_dict(w)
+        ref = other.forward_graphs(xc[:B].contiguous(), one, gz, norm_scope=ECO_NORM_PER_CALL)
+        assert torch.equal(q, ref), B
