@@ -961,19 +961,22 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
     // launch: its per-fragment scales and splits sit after the barrier, on the critical path.
     const int total = (fh_wgrad ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
     int nbig = 0;
-    double rows = 0.0;
+    double rows = 0.0, rows_small = 0.0;
     for (int j = 0; j < n; ++j) {
-      nbig += J.j[j].K1 + J.j[j].K2 == 128;
+      const bool big = J.j[j].K1 + J.j[j].K2 == 128;
+      nbig += big;
       rows += J.j[j].R;
+      if (!big) rows_small += J.j[j].R;
     }
     J.first[0] = 0;
     for (int j = 0; j < n; ++j) {
       const bool big = J.j[j].K1 + J.j[j].K2 == 128;
-      // in proportion to the job's rows: every job issues the same loads per row (dead X columns read column 0
-      // of the row), so a row costs about the same in every job; the per-graph readout job (R = batch) gets one
+      // in proportion to the job's rows (a row costs about the same in every job); the per-graph readout job
+      // (R = batch) gets one
       int g = (int)(total * (double)J.j[j].R / rows);
       if (even_wg) g = total / n;
-      if (big_wg > 0 && nbig > 0 && nbig < n) g = big ? big_wg : (total - nbig * big_wg) / (n - nbig);
+      if (big_wg > 0 && nbig > 0 && nbig < n)  // A/B: big_wg for each K = 128 job, the rest by rows
+        g = big ? big_wg : (int)((total - nbig * big_wg) * (double)J.j[j].R / rows_small);
       J.nwgj[j] = std::max(1, std::min(WG_PER_JOB, g));
       J.first[j + 1] = J.first[j] + J.nwgj[j];
     }
