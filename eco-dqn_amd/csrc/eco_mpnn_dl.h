@@ -23,8 +23,12 @@
 
 namespace eco {
 
-constexpr int DL_NW = 8;                          // waves per workgroup
-constexpr int DL_MT = 4;                          // 16-node tiles per wave
+#ifndef DL_NW_X
+#define DL_NW_X 8  // A/B knob (with DL_MT_X = 32 / DL_NW_X): waves per workgroup
+#define DL_MT_X 4
+#endif
+constexpr int DL_NW = DL_NW_X;                    // waves per workgroup
+constexpr int DL_MT = DL_MT_X;                    // 16-node tiles per wave
 constexpr int DL_MAX_ROWS = DL_NW * DL_MT * 16;   // 512
 constexpr int DL_KC = DL_MAX_ROWS / 32;           // k-chunks of 32 nodes
 constexpr int DL_AW = 8;                          // adjacency words per (node, lane quarter): 16 chunks x 16 bits
