@@ -1153,6 +1153,45 @@ static KCfg pick_cfg(int N, int gpb, bool backward) {
   return c;
 }
 
+extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_b, int32_t n_obs_in,
+                                     const eco_graph_set* gs, const int32_t* graph_ids, int32_t batch,
+                                     const float* obs_x, int32_t norm_scope, float* q_a, const eco_act_config* act_a,
+                                     int32_t* actions_a, float* q_b, const eco_act_config* act_b, int32_t* actions_b,
+                                     void* workspace, eco_stream_t stream) {
+  if (!packed_b) return fail(ECO_ERR_ARG, "null argument");
+  MpnnArgs a;
+  int rc = prepare(a, packed_a, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope);
+  if (rc) return rc;
+  if (!workspace) return fail(ECO_ERR_ARG, "null workspace");
+  if ((act_a && !actions_a) || (act_b && !actions_b)) return fail(ECO_ERR_ARG, "act config without actions buffer");
+  if ((!q_a && !act_a) || (!q_b && !act_b)) return fail(ECO_ERR_ARG, "nothing to compute (q and act both null)");
+  static const bool no_pair = getenv("ECO_MPNN_NO_PAIR") != nullptr;  // A/B knob: two launches
+  if (no_pair || !(a.xw == 8 && dense_eligible(gs, a.gpb) && a.gpb == 1 && gs->adjbits && !getenv("ECO_MPNN_NO_DENSE") &&
+                   !getenv("ECO_DENSE_V1"))) {
+    rc = eco_mpnn_forward(packed_a, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope, q_a, act_a, actions_a, nullptr,
+                          workspace, stream);
+    if (rc) return rc;
+    return eco_mpnn_forward(packed_b, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope, q_b, act_b, actions_b,
+                            nullptr, workspace, stream);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  int* cmax = (int*)workspace;
+  a.call_maxdeg = cmax;
+  a.sv = nullptr;
+  MpnnArgs b = a;
+  a.q = q_a;
+  a.has_act = act_a != nullptr;
+  if (act_a) a.act = *act_a;
+  a.actions = actions_a;
+  b.P = packed_b;
+  b.q = q_b;
+  b.has_act = act_b != nullptr;
+  if (act_b) b.act = *act_b;
+  b.actions = actions_b;
+  if (norm_scope == ECO_NORM_PER_CALL) call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
+  return mpnn_forward_dense2_pair_launch(a, b, st);
+}
+
 extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
                                 const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope,
                                 float* q, const eco_act_config* act, int32_t* actions, void* saved, void* workspace,

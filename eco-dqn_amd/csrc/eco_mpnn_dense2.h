@@ -344,9 +344,13 @@ __device__ __forceinline__ void d2_stage(const MpnnArgs& a, int blk, int rows_pa
 
 // LDS (ECO_D2_LDS): sPL the 2 fp16 planes (the readout's fp32 h3 rows at the end) | sW0, sW1, sW2 32-KB Linear
 //      fragment buffers (sW1 / sW2 hold the V planes of the edge layer; sW1 is the readout scratch) | TE | RI | GB | MD
-template <bool SAVE>
-__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(MpnnArgs a) {
+// NNET = 2 (one graph per block, no saved activations): the block runs TWO networks on the same graphs and node
+// features -- the online and the target network on a train step's s' -- a0 then a1, sharing the staging (graph
+// id -> degrees, adjacency words; node features), with a1's Wf DMA'd while a0's readout runs.
+template <bool SAVE, int NNET>
+__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(MpnnArgs a0, MpnnArgs a1) {
   ECO_D2_LDS;
+  const MpnnArgs& a = a0;  // the staging reads the graph fields, equal in a0 and a1
   ECO_TS(0);
   constexpr int NW = DN_NW;
   constexpr int NT = 64 * NW;
@@ -401,6 +405,17 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
   const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+#pragma unroll
+  for (int net = 0; net < NNET; ++net) {
+  const MpnnArgs& a = net == 0 ? a0 : a1;  // this network's weights and outputs
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  if (net > 0) {  // the 8-input Linears' weights and w_a of this network
+    lin8_load(P + PK_WX, lane, wx8);
+    lin8_load(P + PK_W0, lane, w08);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
+  }
   zero_pad_rows2<NT>(PL, PL1, rows_pad);
   zero_pad_rows2<NT>(WB1, WB2, rows_pad);  // V planes
 
@@ -577,6 +592,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
     lds_barrier();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
     ECO_TS(5 + layer);
   }
+  if (net + 1 < NNET)  // the next network's Wf into the free buffer, landing while this readout runs
+    glds_frags<NW>(WB0, reinterpret_cast<const uint16_t*>(a1.P + PK_FH) + FH_WF, 16, w, lane);
 
   // ---- phase E: readout (mpnn.py:143-159) + act ----
   if (a.gpb == 1) {
@@ -650,7 +667,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
       }
     }
     ECO_TS(8);
-    return;
+    if (net + 1 < NNET) lds_barrier();  // wave 0's readout scratch (the plane array) before the next planes
+    continue;
   }
   // several graphs per block: h3 rows staged as fp32 [rows][D2_HS_LD] in the plane array
   float* Hs = reinterpret_cast<float*>(sPL);
@@ -664,6 +682,8 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense2_kernel(Mpnn
   if (!split && readout_scratch_floats(rows_pad, a.gpb, NW, false) * 4 > D2_WBUF_BYTES) return;  // launch checks
   readout_act<SAVE, NW>(a, Hs, D2_HS_LD, Scr, split, blk, g_valid, rows_valid, R0, RT);
   ECO_TS(8);
+  if (net + 1 < NNET) lds_barrier();
+  }  // networks
 }
 
 static int dense2_check(const MpnnArgs& a) {
@@ -677,9 +697,16 @@ static int dense2_check(const MpnnArgs& a) {
 static int mpnn_forward_dense2_launch(const MpnnArgs& a, bool save, hipStream_t st) {
   if (const int rc = dense2_check(a)) return rc;
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  if (save) mpnn_forward_dense2_kernel<true><<<blocks, 64 * DN_NW, 0, st>>>(a);
-  else mpnn_forward_dense2_kernel<false><<<blocks, 64 * DN_NW, 0, st>>>(a);
+  if (save) mpnn_forward_dense2_kernel<true, 1><<<blocks, 64 * DN_NW, 0, st>>>(a, a);
+  else mpnn_forward_dense2_kernel<false, 1><<<blocks, 64 * DN_NW, 0, st>>>(a, a);
   return check_launch("mpnn_forward_dense2");
+}
+// two networks on the same graphs and features in one launch (a and b differ only in P, q, act, actions)
+static int mpnn_forward_dense2_pair_launch(const MpnnArgs& a, const MpnnArgs& b, hipStream_t st) {
+  if (const int rc = dense2_check(a)) return rc;
+  if (a.gpb != 1) return fail(ECO_ERR_ARG, "paired dense forward: one graph per block only");
+  mpnn_forward_dense2_kernel<false, 2><<<a.B, 64 * DN_NW, 0, st>>>(a, b);
+  return check_launch("mpnn_forward_dense2_pair");
 }
 
 

@@ -87,6 +87,9 @@ _SIG = {
     "eco_mpnn_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_mpnn_forward": (ctypes.c_int, [_P, _I, ctypes.POINTER(GraphSet), _P, _I, _P, _I, _P,
                                         ctypes.POINTER(ActConfig), _P, _P, _P, _P]),
+    "eco_mpnn_forward_pair": (ctypes.c_int, [_P, _P, _I, ctypes.POINTER(GraphSet), _P, _I, _P, _I, _P,
+                                             ctypes.POINTER(ActConfig), _P, _P, ctypes.POINTER(ActConfig), _P, _P,
+                                             _P]),
     "eco_mpnn_saved_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_mpnn_backward_workspace_bytes": (ctypes.c_size_t, [_I, _I]),
     "eco_mpnn_backward": (ctypes.c_int, [_P, _I, ctypes.POINTER(GraphSet), _P, _I, _P, _P, _P, _P, _P, _P]),

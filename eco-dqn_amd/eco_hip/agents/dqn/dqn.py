@@ -252,9 +252,8 @@ class DQN:
         greedy = _lib.ActConfig(0.0, int(self.acting_in_reversible_spin_env), float(self.allowed_value), 0, 0)
         if self.double_dqn:
             # greedy_actions = network(s').argmax (masked for irreversible envs), q_t = target(s')[a*]
-            net.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, act=greedy,
-                               actions_out=self.a_star)
-            tgt.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_tn)
+            net.forward_pair_graphs(tgt, xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, act=greedy,
+                                    actions_out=self.a_star, q_out_other=self.q_tn)
         else:
             tgt.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_tn,
                                act=greedy, actions_out=self.a_star)

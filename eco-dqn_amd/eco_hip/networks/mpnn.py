@@ -138,6 +138,37 @@ class MPNN(torch.nn.Module):
             self.timer.append((ev[0], ev[1], B, graph_ids))
         return q_out
 
+    def forward_pair_graphs(self, other, obs_x, graphs, graph_ids, norm_scope=_lib.ECO_NORM_PER_GRAPH, q_out=None,
+                            act=None, actions_out=None, q_out_other=None, act_other=None, actions_out_other=None,
+                            stream=None):
+        """This network and `other` on the same graphs and node features (the double-DQN pair of
+        dqn.py:416-428: online argmax and target Q on s') -- eco_mpnn_forward_pair: one launch for one-graph
+        dense blocks, else two forwards.  Returns (q_out, q_out_other)."""
+        B, N = obs_x.shape[0], obs_x.shape[1]
+        self._check_x(obs_x)
+        if other.n_obs_in != self.n_obs_in:
+            raise ValueError("paired networks must take the same observables")
+        self._ensure_packed(stream)
+        other._ensure_packed(stream)
+        if q_out is None and act is None:
+            q_out = torch.empty(B, N, dtype=torch.float32, device=obs_x.device)
+        if q_out_other is None and act_other is None:
+            q_out_other = torch.empty(B, N, dtype=torch.float32, device=obs_x.device)
+        gids = graph_ids if graph_ids.dtype == torch.int32 else graph_ids.to(torch.int32)
+        if self.timer is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        _lib.check(_lib.lib.eco_mpnn_forward_pair(
+            _lib.ptr(self.packed), _lib.ptr(other.packed), self.n_obs_in, ctypes.byref(graphs.gs),
+            _lib.ptr(gids.contiguous()), B, _lib.ptr(obs_x), norm_scope, _lib.ptr(q_out),
+            ctypes.byref(act) if act is not None else None, _lib.ptr(actions_out), _lib.ptr(q_out_other),
+            ctypes.byref(act_other) if act_other is not None else None, _lib.ptr(actions_out_other),
+            _lib.ptr(self._workspace(N, B)), _lib.stream_ptr(stream)))
+        if self.timer is not None:
+            ev[1].record()
+            self.timer.append((ev[0], ev[1], 2 * B, graph_ids))  # two forwards' work
+        return q_out, q_out_other
+
     @staticmethod
     def saved_bytes(n_spins, batch):
         return _lib.lib.eco_mpnn_saved_bytes(n_spins, batch)

@@ -227,6 +227,16 @@ int eco_mpnn_forward(const float *packed, int32_t n_obs_in, const eco_graph_set 
                      int32_t batch, const float *obs_x, int32_t norm_scope, float *q, const eco_act_config *act,
                      int32_t *actions, void *saved, void *workspace, eco_stream_t stream);
 
+/* Two networks on the same graphs and node features in one call: the double-DQN pair of dqn.py:416-428
+ * (a = online net -> greedy argmax a* over s', b = target net -> Q(s') to gather at a*).  Equivalent to
+ * eco_mpnn_forward(packed_a, ..., q_a, act_a, actions_a) followed by eco_mpnn_forward(packed_b, ..., q_b,
+ * act_b, actions_b) with saved = NULL; for one-graph dense blocks (ER-200 ... ER-224 with adjbits) it is ONE
+ * launch whose workgroups stage each graph once and run both networks on it. */
+int eco_mpnn_forward_pair(const float *packed_a, const float *packed_b, int32_t n_obs_in, const eco_graph_set *gs,
+                          const int32_t *graph_ids, int32_t batch, const float *obs_x, int32_t norm_scope,
+                          float *q_a, const eco_act_config *act_a, int32_t *actions_a, float *q_b,
+                          const eco_act_config *act_b, int32_t *actions_b, void *workspace, eco_stream_t stream);
+
 /* ---- DQN train step (dqn.py:403-451) ---- */
 
 size_t eco_mpnn_backward_workspace_bytes(int32_t n_spins, int32_t batch);

@@ -160,3 +160,38 @@ def test_dense_large_matches_csr_and_oracle(n, B, kind, param):
     net.forward_graphs(x, store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=q, act=ActConfig(0.0, 1, 0.0, 7, 0),
                        actions_out=acts)
     assert torch.equal(acts.long(), q.argmax(1))
+
+
+@pytest.mark.parametrize("n,B,p", [(200, 300, 0.15), (20, 64, 0.3)])
+def test_forward_pair_matches_two_forwards(n, B, p):
+    """eco_mpnn_forward_pair (the double-DQN s' pair of dqn.py:416-428: online greedy argmax + target Q) against
+    two separate forwards on the same inputs: ER-200 runs the one-launch two-network dense kernel (one graph per
+    block), ER-20 the fallback of two launches.  Bitwise equal Q and actions (the same operations per network)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ActConfig, ECO_NORM_PER_CALL
+    store = GraphStore.random("ER", B, n, p, seed=5)
+    g = torch.Generator().manual_seed(55)
+    wa, wb = mo.init_weights(g, std=0.1), mo.init_weights(g, std=0.1)
+    na, nb = MPNN(device="cuda"), MPNN(device="cuda")
+    na.load_state_dict(wa)
+    nb.load_state_dict(wb)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    gids = torch.randperm(B, generator=g).to(torch.int32).cuda()
+    greedy = ActConfig(0.0, 1, 0.0, 0, 0)
+    a1 = torch.empty(B, dtype=torch.int32, device="cuda")
+    q1 = torch.empty(B, n, device="cuda")
+    qb1 = torch.empty(B, n, device="cuda")
+    na.forward_pair_graphs(nb, xc, store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=q1, act=greedy, actions_out=a1,
+                           q_out_other=qb1)
+    a2 = torch.empty(B, dtype=torch.int32, device="cuda")
+    q2 = torch.empty(B, n, device="cuda")
+    na.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=q2, act=greedy, actions_out=a2)
+    qb2 = nb.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL)
+    assert torch.equal(q1, q2)
+    assert torch.equal(a1, a2)
+    assert torch.equal(qb1, qb2)
+    assert torch.equal(a1.long(), q1.argmax(1))
