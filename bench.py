@@ -167,6 +167,7 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
 
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "final", "train_pmc_hbm.json")
 PMC_SQ = os.path.join(REPO, "profiles", "r03", "final", "pmc_sq_dense.json")
+PMC_PAIRED = True  # the committed train PMC pass ran the paired s' forward (eco_mpnn_forward_pair)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
 # kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
 FWD_NAMES = ("mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
@@ -190,11 +191,12 @@ def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
     try:
         with open(PMC_SQ) as f:
             k = json.load(f)["kernels"]
-        inf = _first(k, [n + "<false>" for n in FWD_NAMES])
-        trn = _first(k, [n + "<true>" for n in FWD_NAMES])
+        inf = _first(k, [n + t for n in FWD_NAMES for t in ("<false, 1>", "<false>")])
+        trn = _first(k, [n + t for n in FWD_NAMES for t in ("<true, 1>", "<true>")])
     except (OSError, ValueError, KeyError):
         return None
-    n_inf, n_trn = 1 + 2 * (B * 2 // M), B * 2 // M  # act + online/target(s') per grad step; online(s) saves
+    n_inf, n_trn = 1 + 2 * (B * 2 // M), B * 2 // M  # act + online/target(s') per grad step (their work, paired
+    # or not); online(s) saves
     busy = (n_inf * inf["mfma_busy"] + n_trn * trn["mfma_busy"]) / (n_inf + n_trn)
     ratio = inf.get("issued_mfma_flop", inf.get("issued_bf16_flop")) / (flops_per_graph * M)
     return {"mfma_busy": busy, "issued_per_algorithmic_flop": ratio, "source": os.path.relpath(PMC_SQ, REPO)}
@@ -228,8 +230,11 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
         if dom == "mpnn_forward_kernel":
             fw = _first(k, FWD_NAMES)
             act, tr = fw[str((B + gpb - 1) // gpb)], fw[str((M + gpb - 1) // gpb)]
-            return (act["hbm_bytes_per_launch"] + 3 * (B * 2 // M) * tr["hbm_bytes_per_launch"]) / \
-                (1 + 3 * (B * 2 // M))
+            # per vector step: one act forward over B graphs, and per gradient step the s' pair (one launch when
+            # paired) + the training forward; tr averages the M-graph launches of the profiled run
+            k = B * 2 // M
+            per_k = 2 if PMC_PAIRED else 3
+            return (act["hbm_bytes_per_launch"] + per_k * k * tr["hbm_bytes_per_launch"]) / (1 + per_k * k)
         bw = _first(k, BWD_NAMES)[str((M + gpb - 1) // gpb)]
         wg = next(iter(_first(k, WGRAD_NAMES).values()))
         return bw["hbm_bytes_per_launch"] + wg["hbm_bytes_per_launch"]
