@@ -152,6 +152,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
 // (each wave-level load is one contiguous 256-B row segment), splits, and writes the three 8-row
 // pieces as 16-B LDS stores into [p][column][row] planes, which are exactly the MFMA fragments
 // (lane l: column l & 31, rows 8 (l >> 5) .. +7 of a 16-row k-step).
+#ifndef WGRAD_DEPTH
+#define WGRAD_DEPTH 2  // register buffers per thread in wgrad_bf3_job (A/B knob)
+#endif
+#ifndef WGRAD_NT
+#define WGRAD_NT 0  // A/B knob: nontemporal (streaming) loads of dY / X in wgrad_bf3_job
+#endif
+#if WGRAD_NT
+#define WG_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define WG_LOAD(p) (*(p))
+#endif
 constexpr int WB_LD = 40;  // bf16 per plane column (32 rows + 8 pad: 80-B stride, conflict-light 16-B reads)
 typedef short bf16x8w __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
@@ -219,11 +230,12 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
   // time makes the compiler wait for every load before the multiply it should overlap)
   auto load_tile = [&](Regs& R, int rb) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
+    for (int k = 0; k < 8; ++k) R.y[k] = WG_LOAD(&ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64]);
 #pragma unroll
     for (int u = 0; u < XU; ++u)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld];
+      for (int k = 0; k < 8; ++k)
+        R.x[u][k] = WG_LOAD(&xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld]);
   };
   auto store_tile = [&](Regs& R, int rb) {
     asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
@@ -283,6 +295,7 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
   };
   // loads are issued unconditionally (rows past r1 clamp to r1 - 1 and are masked at the store): a
   // conditional load makes the compiler drain every tile in flight at the join (vmcnt(0))
+#if WGRAD_DEPTH == 2
   if (r0 < r1) {
     Regs RA, RB;
     load_tile(RA, r0);
@@ -301,6 +314,26 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
       __syncthreads();
     }
   }
+#else  // A/B: D register buffers (3 and 4 measured slower)
+  if (r0 < r1) {
+    constexpr int D = WGRAD_DEPTH;  // register buffers: tiles i+1 .. i+D-1 in flight while tile i is multiplied
+    Regs RB[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_tile(RB[d], r0 + d * WROWS);
+    for (int rb = r0; rb < r1; rb += D * WROWS) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int rt = rb + d * WROWS;
+        if (d > 0 && rt >= r1) break;
+        store_tile(RB[d], rt);
+        __syncthreads();
+        load_tile(RB[d], rt + D * WROWS);
+        compute();
+        __syncthreads();
+      }
+    }
+  }
+#endif
   float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -486,21 +519,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGRAD_FH_WA
     }
   };
   if (r0 < r1) {
-    Regs RA, RB;
-    load_tile(RA, r0);
-    load_tile(RB, r0 + WROWS);
-    for (int rb = r0; rb < r1; rb += 2 * WROWS) {
-      store_tile(RA, rb);
-      __syncthreads();
-      load_tile(RA, rb + 2 * WROWS);
-      compute();
-      __syncthreads();
-      if (rb + WROWS >= r1) break;
-      store_tile(RB, rb + WROWS);
-      __syncthreads();
-      load_tile(RB, rb + 3 * WROWS);
-      compute();
-      __syncthreads();
+    constexpr int D = WGRAD_DEPTH;  // register buffers: tiles i+1 .. i+D-1 in flight while tile i is multiplied
+    Regs RB[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_tile(RB[d], r0 + d * WROWS);
+    for (int rb = r0; rb < r1; rb += D * WROWS) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int rt = rb + d * WROWS;
+        if (d > 0 && rt >= r1) break;
+        store_tile(RB[d], rt);
+        __syncthreads();
+        load_tile(RB[d], rt + D * WROWS);
+        compute();
+        __syncthreads();
+      }
     }
   }
   float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
