@@ -1139,7 +1139,12 @@ extern "C" int eco_replay_compact_sample(const eco_env_config* cfg, const void* 
   const EnvLayout L = env_layout(cfg->n_spins, cfg->max_steps, env_batch);
   const double* tab = (const double*)((const uint8_t*)env_state + L.off_tab + 256);
   const long long P = (long long)capacity + env_batch;
-  replay_compact_sample_kernel<<<dim3(2, m), 256, (size_t)cfg->n_spins * 4, (hipStream_t)stream>>>(
+  // threads per transition: 4096 workgroups of a few nodes' work each are latency chains (ring slot -> graph ->
+  // rows -> count -> features); smaller workgroups keep more of them resident.  ECO_SAMPLE_THREADS: A/B knob
+  static const int nt_env = [] { const char* e = getenv("ECO_SAMPLE_THREADS"); return e ? atoi(e) : 0; }();
+  // (ER-200 x M = 2048: 30.6 / 24.2 / 21.0 us per call at 256 / 128 / 64 threads, profiles/r03/ab/sample_threads_*)
+  const int nt = (nt_env == 64 || nt_env == 128 || nt_env == 256) ? nt_env : (cfg->n_spins <= 256 ? 64 : 128);
+  replay_compact_sample_kernel<<<dim3(2, m), nt, (size_t)cfg->n_spins * 4, (hipStream_t)stream>>>(
       *cfg, compact_carve(const_cast<void*>(ring), cfg->n_spins, P), P, capacity, size, pushed, m,
       rng3(seed, counter, 0x5A5A), tab, *gs, xs, xn, graph_ids, actions, rewards, dones);
   return check_launch("replay_compact_sample");
