@@ -1159,6 +1159,8 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
                                      int32_t* actions_a, float* q_b, const eco_act_config* act_b, int32_t* actions_b,
                                      void* workspace, eco_stream_t stream) {
   if (!packed_b) return fail(ECO_ERR_ARG, "null argument");
+  const bool reuse_maxdeg = norm_scope == ECO_NORM_PER_CALL_REUSE;
+  if (reuse_maxdeg) norm_scope = ECO_NORM_PER_CALL;
   MpnnArgs a;
   int rc = prepare(a, packed_a, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope);
   if (rc) return rc;
@@ -1168,11 +1170,13 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
   static const bool no_pair = getenv("ECO_MPNN_NO_PAIR") != nullptr;  // A/B knob: two launches
   if (no_pair || !(a.xw == 8 && dense_eligible(gs, a.gpb) && a.gpb == 1 && gs->adjbits && !getenv("ECO_MPNN_NO_DENSE") &&
                    !getenv("ECO_DENSE_V1"))) {
-    rc = eco_mpnn_forward(packed_a, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope, q_a, act_a, actions_a, nullptr,
+    rc = eco_mpnn_forward(packed_a, n_obs_in, gs, graph_ids, batch, obs_x,
+                          reuse_maxdeg ? ECO_NORM_PER_CALL_REUSE : norm_scope, q_a, act_a, actions_a, nullptr,
                           workspace, stream);
     if (rc) return rc;
-    return eco_mpnn_forward(packed_b, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope, q_b, act_b, actions_b,
-                            nullptr, workspace, stream);
+    return eco_mpnn_forward(packed_b, n_obs_in, gs, graph_ids, batch, obs_x,
+                            norm_scope == ECO_NORM_PER_GRAPH ? norm_scope : ECO_NORM_PER_CALL_REUSE, q_b, act_b,
+                            actions_b, nullptr, workspace, stream);
   }
   hipStream_t st = (hipStream_t)stream;
   int* cmax = (int*)workspace;
@@ -1188,7 +1192,8 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
   b.has_act = act_b != nullptr;
   if (act_b) b.act = *act_b;
   b.actions = actions_b;
-  if (norm_scope == ECO_NORM_PER_CALL) call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
+  if (norm_scope == ECO_NORM_PER_CALL && !reuse_maxdeg)
+    call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   return mpnn_forward_dense2_pair_launch(a, b, st);
 }
 
@@ -1196,6 +1201,8 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
                                 const int32_t* graph_ids, int32_t batch, const float* obs_x, int32_t norm_scope,
                                 float* q, const eco_act_config* act, int32_t* actions, void* saved, void* workspace,
                                 eco_stream_t stream) {
+  const bool reuse_maxdeg = norm_scope == ECO_NORM_PER_CALL_REUSE;  // the workspace already holds the call max
+  if (reuse_maxdeg) norm_scope = ECO_NORM_PER_CALL;
   MpnnArgs a;
   int rc = prepare(a, packed, n_obs_in, gs, graph_ids, batch, obs_x, norm_scope);
   if (rc) return rc;
@@ -1211,7 +1218,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   a.has_act = act != nullptr;
   if (act) a.act = *act;
   a.actions = actions;
-  if (norm_scope == ECO_NORM_PER_CALL) {
+  if (norm_scope == ECO_NORM_PER_CALL && !reuse_maxdeg) {
     call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) {

@@ -605,21 +605,28 @@ __global__ void colsum_jobs_kernel(ColJobs jobs) {
 // ---------------------------------------------------------------------- TD ----
 // dqn.py:403-440 for a reversible env: q_t = target(s')[argmax online(s')] (double DQN),
 // td = r + (1 - done) * gamma * q_t, loss = mean((q(s,a) - td)^2), dq = dloss/dq.
+// One thread per element of dq[B][N]: the element of the taken action gets the TD gradient (and its row's
+// squared error), every other element zero -- the zero-fill of loss.backward()'s dQ and the TD step in one pass.
 __global__ void td_kernel(const float* q_s, const float* q_tn, const int32_t* a_star, const int32_t* actions,
                           const float* rewards, const float* dones, int B, int N, float gamma, int clip,
                           float* dq, float* sqerr) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)B * N) return;
+  const int b = (int)(i / N), j = (int)(i - (size_t)b * N);
+  int a = actions[b];
+  if ((unsigned)a >= (unsigned)N) a = 0;
+  if (j != a) {
+    dq[i] = 0.f;
+    return;
+  }
   int as = a_star[b];
   if ((unsigned)as >= (unsigned)N) as = 0;  // never index outside the row (all-masked argmax is 0)
   float qt = q_tn[(size_t)b * N + as];
   if (clip && qt < 0.f) qt = 0.f;  // clip_Q_targets (dqn.py:431-432)
   const float td = rewards[b] + (1.f - dones[b]) * gamma * qt;
-  int a = actions[b];
-  if ((unsigned)a >= (unsigned)N) a = 0;
-  const float q = q_s[(size_t)b * N + a];
+  const float q = q_s[i];
   const float diff = q - td;
-  dq[(size_t)b * N + a] = 2.f * diff / (float)B;  // mse_loss(reduction='mean') backward
+  dq[i] = 2.f * diff / (float)B;  // mse_loss(reduction='mean') backward
   sqerr[b] = diff * diff;
 }
 
@@ -1038,10 +1045,9 @@ extern "C" int eco_dqn_td(const float* q_s, const float* q_target_next, const in
     return fail(ECO_ERR_ARG, "null argument");
   if (batch < 1 || n_spins < 1) return fail(ECO_ERR_ARG, "bad batch/n_spins");
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(dq, 0, sizeof(float) * (size_t)batch * n_spins, st) != hipSuccess)
-    return fail(ECO_ERR_HIP, "memset dq failed");
-  td_kernel<<<(batch + 255) / 256, 256, 0, st>>>(q_s, q_target_next, a_star, actions, rewards, dones, batch, n_spins,
-                                                 gamma, clip_q_targets, dq, sqerr);
+  const size_t n = (size_t)batch * n_spins;
+  td_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(q_s, q_target_next, a_star, actions, rewards, dones, batch,
+                                                         n_spins, gamma, clip_q_targets, dq, sqerr);
   mean_kernel<<<1, 256, 0, st>>>(sqerr, batch, loss);
   return check_launch("dqn_td");
 }

@@ -30,7 +30,7 @@ def obs_x_stride(n_obs):
     return 8 if n_obs <= 8 else 16
 ECO_MAX_SPINS = 2048
 ECO_COMPACT_MAX_SPINS = 8192  # include/eco_hip.h: compact replay (sample rebuilds s' in LDS)
-ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL = 0, 1
+ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL, ECO_NORM_PER_CALL_REUSE = 0, 1, 2
 ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
 
 

@@ -254,11 +254,13 @@ class DQN:
             # greedy_actions = network(s').argmax (masked for irreversible envs), q_t = target(s')[a*]
             net.forward_pair_graphs(tgt, xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, act=greedy,
                                     actions_out=self.a_star, q_out_other=self.q_tn)
+            # same graph ids, same workspace: the per-call max degree the pair left there
+            scope_s = _lib.ECO_NORM_PER_CALL_REUSE
         else:
             tgt.forward_graphs(xn, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_tn,
                                act=greedy, actions_out=self.a_star)
-        net.forward_graphs(xs, self.graphs, gid, norm_scope=_lib.ECO_NORM_PER_CALL, q_out=self.q_s,
-                           saved=self.saved)
+            scope_s = _lib.ECO_NORM_PER_CALL
+        net.forward_graphs(xs, self.graphs, gid, norm_scope=scope_s, q_out=self.q_s, saved=self.saved)
         _lib.check(_lib.lib.eco_dqn_td(_lib.ptr(self.q_s), _lib.ptr(self.q_tn), _lib.ptr(self.a_star),
                                        _lib.ptr(act), _lib.ptr(rew), _lib.ptr(done), m, self.N,
                                        ctypes.c_float(self.gamma), int(bool(self.clip_Q_targets)), _lib.ptr(self.dq),

@@ -191,7 +191,10 @@ int eco_mpnn_pack(const float *params, int32_t n_obs_in, float *packed, eco_stre
 
 /* Norm-max scope of EdgeAndNodeEmbeddingLayer (mpnn.py:102): */
 enum { ECO_NORM_PER_GRAPH = 0, /* B=1 semantics: act (dqn.py:282) */
-       ECO_NORM_PER_CALL = 1   /* max over the whole call: train_step / batched eval */ };
+       ECO_NORM_PER_CALL = 1,  /* max over the whole call: train_step / batched eval */
+       ECO_NORM_PER_CALL_REUSE = 2 /* as PER_CALL, the call maximum taken from this workspace as the previous
+                                      PER_CALL forward on the SAME graph ids left it (train_step's online(s)
+                                      after the s' pair): skips its reduction launch */ };
 
 /* epsilon-greedy act fused into the forward (dqn.py:453-465, predict :490-512).
  * action = random with probability epsilon (uniform over allowed vertices),

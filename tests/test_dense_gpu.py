@@ -195,3 +195,35 @@ def test_forward_pair_matches_two_forwards(n, B, p):
     assert torch.equal(a1, a2)
     assert torch.equal(qb1, qb2)
     assert torch.equal(a1.long(), q1.argmax(1))
+
+
+@pytest.mark.parametrize("n,B,p", [(200, 96, 0.15), (20, 64, 0.3), (500, 8, 0.02)])
+def test_norm_per_call_reuse(n, B, p):
+    """ECO_NORM_PER_CALL_REUSE (train_step's online(s) forward after the s' pair on the same graph ids) takes the
+    per-call max degree the previous PER_CALL forward left in the workspace: bitwise the PER_CALL result, with and
+    without saved activations, on the dense, the small-graph and the BA-500-size paths.  After a forward on other
+    graph ids the workspace holds THEIR maximum, which is the documented contract (the reuse is the caller's
+    promise), so the test only checks the same-ids case and that a fresh PER_CALL call restores it."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_CALL, ECO_NORM_PER_CALL_REUSE
+    store = GraphStore.random("ER", B, n, p, seed=7)
+    g = torch.Generator().manual_seed(77)
+    net = MPNN(device="cuda")
+    net.load_state_dict(mo.init_weights(g, std=0.1))
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    gids = torch.randperm(B, generator=g).to(torch.int32).cuda()
+    q_ref = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL).clone()
+    q_re = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL_REUSE).clone()
+    assert torch.equal(q_ref, q_re)
+    saved = torch.empty(net.saved_bytes(n, B), dtype=torch.uint8, device="cuda")
+    q_sv = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL_REUSE, saved=saved).clone()
+    assert torch.equal(q_ref, q_sv)
+    # a different subset of graphs (smaller max degree possible), then the full set again with PER_CALL
+    sub = gids[: max(1, B // 4)].contiguous()
+    net.forward_graphs(xc[: sub.numel()].contiguous(), store, sub, norm_scope=ECO_NORM_PER_CALL)
+    q_again = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL)
+    assert torch.equal(q_ref, q_again)
