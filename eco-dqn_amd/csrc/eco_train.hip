@@ -23,8 +23,15 @@ struct WJob {
   int out_col0;      // first column in the flat buffer
 };
 constexpr int MAX_JOBS = 10;
+#ifndef WGRAD_SWZ
+#define WGRAD_SWZ 0  // A/B knob: wgrad_bf3 planes without padding (XOR-swizzled 16-B chunks): 37 KB, 4 per CU
+#endif
 #ifndef WGRAD_WG_X
+#if WGRAD_SWZ
+#define WGRAD_WG_X 4
+#else
 #define WGRAD_WG_X 3  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
+#endif
 #endif
 #ifndef WGRAD_FH_WG_X
 #define WGRAD_FH_WG_X 3  // wgrad_fh_kernel: workgroups per CU over all jobs (27 KB LDS each)
@@ -163,7 +170,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
 #else
 #define WG_LOAD(p) (*(p))
 #endif
+#if WGRAD_SWZ
+// bf16 per plane column (32 rows, no pad): the 16-B row chunk k of column c is stored at chunk k ^ ((c >> 2) & 3), so
+// the 16 consecutive columns of a 16-lane ds_read / ds_write_b128 group hit 16 distinct 4-bank groups
+constexpr int WB_LD = 32;
+#define WB_CH(k, c) ((k) ^ (((c) >> 2) & 3))
+#else
 constexpr int WB_LD = 40;  // bf16 per plane column (32 rows + 8 pad: 80-B stride, conflict-light 16-B reads)
+#define WB_CH(k, c) (k)
+#endif
 typedef short bf16x8w __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
 
@@ -241,35 +256,44 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
     asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
 #pragma unroll
     for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
-    split8_store(sY + yc * WB_LD + 8 * yg, PY, R.y);
+    split8_store(sY + yc * WB_LD + 8 * WB_CH(yg, yc), PY, R.y);
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         R.x[u][k] = rb + 8 * (xg0 + XG * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
-      split8_store(sX + xc * WB_LD + 8 * (xg0 + XG * u), PX, R.x[u]);
+      split8_store(sX + xc * WB_LD + 8 * WB_CH(xg0 + XG * u, xc), PX, R.x[u]);
     }
   };
   // this wave's output tiles: t = w + 4q -> o-tile w & 1, i-tiles (w >> 1) and (w >> 1) + 2
   const int ot = w & 1;
   const bool live0 = w < ntile, live1 = w + 4 < ntile;
+#if WGRAD_SWZ
+  // k-step s reads row chunk 2s + h of the lane's column (every column this lane reads has the same (c >> 2) & 3)
+  const int so[2] = {8 * WB_CH(h, jj), 8 * WB_CH(2 + h, jj)};
+  const uint16_t* ya = sY + (32 * ot + jj) * WB_LD;
+  const uint16_t* xb0 = sX + (32 * (w >> 1) + jj) * WB_LD;
+#define WB_OFF(s) so[s]
+#else
   const uint16_t* ya = sY + (32 * ot + jj) * WB_LD + 8 * h;
   const uint16_t* xb0 = sX + (32 * (w >> 1) + jj) * WB_LD + 8 * h;
+#define WB_OFF(s) (16 * (s))
+#endif
   const uint16_t* xb1 = xb0 + 64 * WB_LD;
   auto compute = [&]() {
   if (live0) {
 #pragma unroll
     for (int s = 0; s < WROWS / 16; ++s) {
-      const bf16x8w a1 = *reinterpret_cast<const bf16x8w*>(ya + 16 * s);
-      const bf16x8w a2 = *reinterpret_cast<const bf16x8w*>(ya + PY + 16 * s);
-      const bf16x8w a3 = *reinterpret_cast<const bf16x8w*>(ya + 2 * PY + 16 * s);
-      const bf16x8w b1 = *reinterpret_cast<const bf16x8w*>(xb0 + 16 * s);
-      const bf16x8w b2 = *reinterpret_cast<const bf16x8w*>(xb0 + PX + 16 * s);
-      const bf16x8w b3 = *reinterpret_cast<const bf16x8w*>(xb0 + 2 * PX + 16 * s);
+      const bf16x8w a1 = *reinterpret_cast<const bf16x8w*>(ya + WB_OFF(s));
+      const bf16x8w a2 = *reinterpret_cast<const bf16x8w*>(ya + PY + WB_OFF(s));
+      const bf16x8w a3 = *reinterpret_cast<const bf16x8w*>(ya + 2 * PY + WB_OFF(s));
+      const bf16x8w b1 = *reinterpret_cast<const bf16x8w*>(xb0 + WB_OFF(s));
+      const bf16x8w b2 = *reinterpret_cast<const bf16x8w*>(xb0 + PX + WB_OFF(s));
+      const bf16x8w b3 = *reinterpret_cast<const bf16x8w*>(xb0 + 2 * PX + WB_OFF(s));
       if (live1) {
-        const bf16x8w c1 = *reinterpret_cast<const bf16x8w*>(xb1 + 16 * s);
-        const bf16x8w c2 = *reinterpret_cast<const bf16x8w*>(xb1 + PX + 16 * s);
-        const bf16x8w c3 = *reinterpret_cast<const bf16x8w*>(xb1 + 2 * PX + 16 * s);
+        const bf16x8w c1 = *reinterpret_cast<const bf16x8w*>(xb1 + WB_OFF(s));
+        const bf16x8w c2 = *reinterpret_cast<const bf16x8w*>(xb1 + PX + WB_OFF(s));
+        const bf16x8w c3 = *reinterpret_cast<const bf16x8w*>(xb1 + 2 * PX + WB_OFF(s));
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, c1, acc[1], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[0], 0, 0, 0);
