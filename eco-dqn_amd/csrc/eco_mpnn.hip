@@ -56,22 +56,35 @@ namespace eco {
 
 // Per-matrix power-of-two scale of the fp16x2 Linear pieces (PK_FHS, eco_mpnn.h): one block per matrix
 // (Wf, then Wm / Wu of each layer); kw puts max |w| 2^kw into [2^14, 2^15).
-__global__ __launch_bounds__(256) void pack_scale_kernel(const float* __restrict__ f, int nobs, float* __restrict__ p) {
+__device__ __forceinline__ float wave_fmax(float v) {  // fmaxf over the wave (NaNs dropped, as fmaxf does)
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x128, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x122, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x121, 0xF, 0xF, false)));
+  auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(s16[0]), __uint_as_float(s16[1]));
+  auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(s32[0]), __uint_as_float(s32[1]));
+}
+
+// Per-matrix power-of-two scale of the fp16x2 Linear pieces (PK_FHS, eco_mpnn.h): one block per matrix
+// (Wf, then Wm / Wu of each layer); kw puts max |w| 2^kw into [2^14, 2^15).  1024 threads, wave maxima.
+constexpr int PS_THREADS = 1024;
+__global__ __launch_bounds__(PS_THREADS) void pack_scale_kernel(const float* __restrict__ f, int nobs,
+                                                                 float* __restrict__ p) {
   const FlatOffsets o = flat_offsets(nobs);
   const int m = blockIdx.x;
   const float* W = m == 0 ? f + o.Wf : f + o.L + (m - 1) * 8192;
   const int n = m == 0 ? 4096 : 8192;
   float mx = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) mx = fmaxf(mx, fabsf(W[i]));
-  __shared__ float red[256];
-  red[threadIdx.x] = mx;
+  for (int i = threadIdx.x; i < n; i += PS_THREADS) mx = fmaxf(mx, fabsf(W[i]));
+  mx = wave_fmax(mx);
+  __shared__ float red[PS_THREADS / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    const float v = red[0];
+    float v = 0.f;
+    for (int k = 0; k < PS_THREADS / 64; ++k) v = fmaxf(v, red[k]);
     const int kw = (v > 0.f && v < INFINITY) ? 15 - __builtin_amdgcn_frexp_expf(v) : 0;
     p[PK_FHS + m] = __int_as_float(kw);
   }
@@ -1074,7 +1087,7 @@ extern "C" size_t eco_mpnn_packed_count(void) { return (size_t)PK_TOTAL; }
 extern "C" int eco_mpnn_pack(const float* params, int32_t n_obs_in, float* packed, eco_stream_t stream) {
   if (!params || !packed) return fail(ECO_ERR_ARG, "null params/packed");
   if (n_obs_in < 1 || n_obs_in > ECO_MPNN_MAX_OBS) return fail(ECO_ERR_ARG, "n_obs_in out of range [1, 16]");
-  pack_scale_kernel<<<FH_NMAT, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
+  pack_scale_kernel<<<FH_NMAT, PS_THREADS, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   pack_kernel<<<(PK_TOTAL + 255) / 256, 256, 0, (hipStream_t)stream>>>(params, n_obs_in, packed);
   return check_launch("mpnn_pack");
 }
