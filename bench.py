@@ -17,7 +17,11 @@ train loop all-reduces gradients over RCCL (weak scaling, B fixed per GPU).
 Prints ONE JSON line on rank 0 with
   roofline: dominant kernel measured live with HIP events (on the launch stream),
             algorithmic FLOPs from SURVEY.md 8d: forward F = 1392*nnz + 107,648*N + 8,192
-            per graph, backward = 2F; peak = dense f32-input MFMA (157.3 TFLOP/s).
+            per graph, backward = 2F; peak = the dense peak of the MFMA dtype the kernel ISSUES
+            (f16 / bf16, 2.5 PFLOP/s: the fp16x2 / bf16x3 split kernels), frac <= 1 by construction;
+            the f32-MFMA figure (157.3) is kept as a separately named field.
+  env_step_roofline: the env step kernel alone (same B, N), SURVEY.md 8d incremental algorithmic bytes
+            per env-step (N + 14.25 N + 28 N) x rate / HBM peak (8 TB/s).
   cpu_baseline: the oracle ('port') env + torch-CPU MPNN act loop on this host.
 """
 import argparse
@@ -34,6 +38,23 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak ~8 TB/s
+
+
+def envstep_alg_bytes(n):
+    """SURVEY.md 8d algorithmic HBM bytes of one incremental env-step: one column of J (N), the episode
+    state read + written (spins N, h 4N, tsf 2N, best bitset N/8: 14.25N) and the fp32 observation rows
+    (7 x 4 B = 28N)."""
+    return n + 14.25 * n + 28.0 * n
+
+
+def envstep_roofline(rate, ms, n):
+    """env_step_roofline object from a measured env-step rate (env-steps/s) and mean launch time."""
+    bpe = envstep_alg_bytes(n)
+    achieved = bpe * rate / 1e9
+    return {"bound": "hbm", "kernel": "env_step_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "alg_bytes_per_env_step": bpe, "env_steps_per_s": rate,
+            "avg_launch_ms": ms, "source": "SURVEY.md 8d incremental bytes x the env step kernel's rate "
+                                          "(HIP events, random actions, same B and N)"}
 
 
 def mpnn_flops(nnz, n):
@@ -169,6 +190,27 @@ PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "final", "train_pmc_hbm.json
 PMC_SQ = os.path.join(REPO, "profiles", "r03", "final", "pmc_sq_dense.json")
 PMC_PAIRED = True  # the committed train PMC pass ran the paired s' forward (eco_mpnn_forward_pair)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
+
+
+def forward_kernel_name(n, graph, n_graphs=None):
+    """The forward kernel the dispatcher runs for 8-feature rows and +-1 / unit weights (eco_mpnn_forward):
+    blocks of <= 224 rows -> the fp16x2 dense kernels; one graph of 224 < N <= 512 -> the fp16x2 DL kernels;
+    N > 512 on one shared graph -> the shared-graph kernels (bf16x3 Linears).  All issue f16/bf16 MFMAs."""
+    if n <= 224:
+        return "mpnn_forward_dense2_kernel"
+    if n <= 512:
+        return "mpnn_forward_dl_kernel"
+    return "shared_agg_kernel+shared_lin_kernel" if n_graphs == 1 else "mpnn_forward_large_kernel"
+
+
+def mfma_roofline(achieved_tflops, kernel):
+    """roofline fields for an MPNN kernel: frac against the dense peak of the MFMA dtype it issues (f16 for
+    the fp16x2 dense / DL kernels, bf16 for the bf16x3 shared-graph Linears, both 2.5 PF; f32 157.3 TF for the
+    per-episode large kernel's f32 MFMAs is not used there either: it also runs bf16x3 fragments)."""
+    peak = F16_MFMA_PEAK_TFLOPS
+    return {"bound": "mfma", "kernel": kernel, "achieved": achieved_tflops, "peak": peak, "unit": "TFLOP/s",
+            "frac": achieved_tflops / peak, "peak_dtype": "f16/bf16 dense MFMA (the issued dtype)",
+            "frac_vs_f32_mfma_peak": achieved_tflops / FP32_MFMA_PEAK_TFLOPS}
 # kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
 FWD_NAMES = ("mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
 BWD_NAMES = ("mpnn_backward_dense2_kernel", "mpnn_backward_dense_kernel")
@@ -242,14 +284,15 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
         return None
 
 
-def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234):
-    """The batched MaxCut env step kernel alone (spinsystem.py:355-559, ER(n, 0.15) +-1 graphs, one per
-    episode, uniform random actions drawn beforehand): env-steps/s over `steps` launches timed with HIP
-    events on the launch stream, and the mean launch time (ms)."""
+def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234, store=None):
+    """The batched MaxCut env step kernel alone (spinsystem.py:355-559, ER(n, 0.15) +-1 graphs -- or the
+    given store's graphs -- one per episode, uniform random actions drawn beforehand): env-steps/s over
+    `steps` launches timed with HIP events on the launch stream, and the mean launch time (ms)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget
-    store = GraphStore.random("ER", B, n, 0.15, seed=seed, device=dev)
+    if store is None:
+        store = GraphStore.random("ER", B, n, 0.15, seed=seed, device=dev)
     T = 2 * n
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
@@ -270,6 +313,40 @@ def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234):
     env.check_errors()
     ms = e0.elapsed_time(e1) / steps
     return B / (ms * 1e-3), ms
+
+
+def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000):
+    """What the timed vector steps never contain (T = 2N steps per episode, 20 timed steps): the full reset of
+    all B episodes at an episode boundary (fresh spins, compact-replay snapshot; dqn.py:306-327), and one
+    evaluate_agent() at the reference's ER-200 test settings (train_eco.py:59-69,166-169,368-377: 50 test graphs,
+    BEST metric, every 50k env-steps).  Both measured here with HIP-synchronised wall time and amortised per
+    vector step: reset / T, evaluation x (B x world / test_frequency)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.agents.dqn.utils import TestMetric
+    env, T, n = agent.env, agent.env.max_steps, agent.N
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agent._reset_env(np.arange(B) % agent.graphs.n_graphs, agent.seed + 99)
+    torch.cuda.synchronize()
+    reset_ms = (time.perf_counter() - t0) * 1e3
+    test = VecSpinSystem(GraphStore.random("ER", test_graphs, n, 0.15, seed=4321, device=dev), 64, T,
+                         **env.env_args)
+    saved = (agent.test_envs, agent.test_episodes, agent.test_metric)
+    agent.test_envs, agent.test_episodes, agent.test_metric = test, test_graphs, TestMetric.BEST
+    agent.evaluate_agent()  # first call: allocations
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agent.evaluate_agent()
+    torch.cuda.synchronize()
+    eval_ms = (time.perf_counter() - t0) * 1e3
+    agent.test_envs, agent.test_episodes, agent.test_metric = saved
+    per_vec = reset_ms / T + eval_ms * (B * world / test_frequency)
+    return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T,
+            "evaluate_agent_ms": eval_ms, "evaluate_every_env_steps": test_frequency,
+            "evaluate_setting": f"{test_graphs} ER-{n} test graphs, BEST metric, {T} greedy steps each",
+            "amortised_ms_per_vector_step": per_vec,
+            "note": "not in the timed region: amortised, these would add this many ms to ms_per_step"}
 
 
 def _free_port():
@@ -478,6 +555,8 @@ def main():
     dt = max_over_ranks(dt_rank, device=dev)
     pg = process_group_info(world, dt_rank, args.steps, local, dev)
 
+    fixed = untimed_costs(agent, B, world, dev) if train else None
+
     # per-kernel roofline from the live events: forward launches vs backward launches
     kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}
     mean_gf = float(gflops.mean())  # sampled minibatches draw from this pool: use its mean per graph
@@ -519,15 +598,18 @@ def main():
                        "replay_ratio": 2.0, "lr": lr, "target_sync": "every %d gradient steps"
                        % agent.target_sync_grad_steps,
                        "parallelism": f"episodes sharded, dp{world} grad all-reduce"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, %s)" % os.path.relpath(PMC_SUMMARY, REPO),
-                         "avg_launch_ms": avg_ms, "launches": cnt,
-                         "flops_per_launch": fl / max(cnt, 1)},
+            "roofline": dict(mfma_roofline(achieved, forward_kernel_name(n, args.graph)
+                                           if dom == "mpnn_forward_kernel" else dom),
+                         traffic=pmc_traffic(dom, B, args.minibatch, n, args.graph) if train else None,
+                         traffic_unit="HBM bytes per launch (PMC, %s)" % os.path.relpath(PMC_SUMMARY, REPO),
+                         avg_launch_ms=avg_ms, launches=cnt, flops_per_launch=fl / max(cnt, 1)),
             "kernels_ms_per_step": {k: v[0] / args.steps for k, v in kern.items()},
             "process_group": pg,
         }
+        # the env step kernel alone on this bench's graphs: SURVEY.md 8d's HBM roofline of the env step
+        es_rate, es_ms = envstep_rate(dev, B, n, store=store)
+        out["env_step_roofline"] = envstep_roofline(es_rate, es_ms, n)
+        out["untimed_per_episode_costs"] = fixed
         mf = pmc_mfma(dom, B, args.minibatch, n, args.graph, mean_gf) if train else None
         if mf:
             issued = achieved * mf["issued_per_algorithmic_flop"]
@@ -537,7 +619,6 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline_learn_loop"] = cpu_baseline(n, train=train)
             if args.graph == "ER":
-                es_rate, es_ms = envstep_rate(dev, B, n)
                 out["cpu_baseline"] = cpu_refcost_baseline(n, gpus_on_node=torch.cuda.device_count())
                 cb = out["cpu_baseline"]
                 # like for like: env step vs env step (rollout, random policy) and learn loop vs learn loop
@@ -625,16 +706,15 @@ def inference_bench(args, world, rank, local, dev, dist):
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32 (MPNN on f32-exact MFMA / bf16x3 splits) / f64+int (env)",
+            "dtype": ("f32-accurate MPNN on f16 MFMA (fp16x2 splits)" if n <= 512 else
+                      "f32-accurate MPNN on bf16 MFMA (bf16x3 splits)") + " / f64+int (env)",
             "data": "synthetic: seeded graphs; random-init MPNN (std 0.1)",
             "config": {"workload": f"{name} x{B} episodes/GPU: MPNN fwd + greedy act + env step "
                                    f"({'configs[4]' if args.workload == 'gset' else 'configs[1]'})",
                        "n_spins": n, "envs_per_gpu": B, "graphs": ngraphs, "max_steps": T,
                        "parallelism": f"episodes sharded, dp{world}, no collective until the best-cut reduce"},
-            "roofline": {"bound": "mfma", "kernel": "mpnn_forward", "achieved": fl / (fwd_ms * 1e-3) / 1e12,
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": fl / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                         "avg_launch_ms": fwd_ms, "flops_per_launch": fl},
+            "roofline": dict(mfma_roofline(fl / (fwd_ms * 1e-3) / 1e12, forward_kernel_name(n, kind, ngraphs)),
+                             traffic=None, avg_launch_ms=fwd_ms, flops_per_launch=fl),
             "best_cut_after_steps": best_cut,
             "process_group": pg,
         }

@@ -522,9 +522,16 @@ int eco::graphs_prepare_range(eco_graph_set* gs, int first, int count, hipStream
                               (int)lds);
     graphs_prepare_kernel<1><<<(count + GP_WAVES - 1) / GP_WAVES, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
   } else {
+    // one workgroup per graph holds row pointers, row sums and nonzero counts in LDS: 12 B per vertex,
+    // so the graph set may have at most 160 KB / 12 B = 13,653 vertices (every env kernel stops at
+    // ECO_MAX_SPINS = 2048 anyway); larger sets are rejected here rather than failing at launch
     const size_t lds = (size_t)(3 * gs->n_spins + 1) * sizeof(int);
-    (void)hipFuncSetAttribute((const void*)graphs_prepare_kernel<GP_WAVES>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lds > (size_t)160 * 1024)
+      return fail(ECO_ERR_ARG, "graphs_prepare: n_spins = " + std::to_string(gs->n_spins) +
+                                   " needs " + std::to_string(lds) + " B of LDS (> 160 KB): at most 13653 vertices");
+    if (hipFuncSetAttribute((const void*)graphs_prepare_kernel<GP_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return fail(ECO_ERR_HIP, "graphs_prepare: cannot raise the dynamic LDS limit");
     graphs_prepare_kernel<GP_WAVES><<<count, 64 * GP_WAVES, lds, st>>>(*gs, first, count);
   }
   int rc = check_launch("graphs_prepare");

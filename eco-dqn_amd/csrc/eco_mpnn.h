@@ -147,11 +147,13 @@ inline int device_cu_count() {
   }();
   return cus;
 }
+#ifndef ECO_AB_GPB
+#define ECO_AB_GPB 0  // A/B builds only (tools/): force this many graphs per block
+#endif
 inline int graphs_per_block(int N, int B) {
-  static const int cap = [] { const char* e = getenv("ECO_MPNN_GPB"); return e ? atoi(e) : 0; }();  // A/B knob
   const int cus = device_cu_count();
   const int gmax = N >= 208 ? 1 : 208 / N;
-  if (cap > 0) return cap < gmax ? cap : gmax;
+  if (ECO_AB_GPB > 0) return ECO_AB_GPB < gmax ? ECO_AB_GPB : gmax;
   int best = gmax;
   double best_cost = 1e300;
   for (int g = gmax; g >= 1 && 2 * g >= gmax; --g) {
@@ -168,6 +170,9 @@ int adjbits_build(const eco_graph_set* gs, int first, int count, hipStream_t st)
 inline bool adjbits_applies(int n_spins) { return n_spins > 104 && n_spins <= 512; }
 // u32 words of gs->adjbits per node: 4 lane quarters x (4 words up to 224 vertices, 8 above)
 inline int adjbits_words_per_node(int n_spins) { return n_spins <= 224 ? 16 : 32; }
+
+// kernel-path policy (eco_set_kernel_paths, include/eco_hip.h): ECO_PATH_* bits, process-wide
+int kernel_paths();
 
 size_t mpnn_grad_ws_bytes(int32_t n_spins, int32_t batch);
 int mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_graph_set* gs, const int32_t* graph_ids,

@@ -19,6 +19,7 @@
 #include "eco_mpnn.h"
 #include "eco_mpnn_dev.h"
 
+#include <atomic>
 #include <cstdlib>
 
 namespace eco {
@@ -1111,6 +1112,16 @@ extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
   return sv_mask_offset_floats(RT, batch) * sizeof(float) + RT * 4 * SM_TENSORS * sizeof(uint16_t);
 }
 
+#ifndef ECO_AB_NW
+#define ECO_AB_NW 0  // A/B builds only (tools/): force the CSR kernels' wave count
+#endif
+static std::atomic<int> g_kernel_paths{0};
+int eco::kernel_paths() { return g_kernel_paths.load(std::memory_order_relaxed); }
+
+extern "C" int32_t eco_set_kernel_paths(int32_t mask) {
+  return g_kernel_paths.exchange(mask & (ECO_PATH_NO_DENSE | ECO_PATH_NO_DL | ECO_PATH_NO_SHARED | ECO_PATH_NO_PAIR));
+}
+
 struct KCfg {
   int nw, maxt;
   bool wlds;
@@ -1137,10 +1148,7 @@ static KCfg pick_cfg(int N, int gpb, bool backward) {
   const int rows_pad = (gpb * N + 15) & ~15;
   const int ntiles = rows_pad / 16;
   KCfg c;
-  static const int force_nw = [] {
-    const char* e = getenv("ECO_MPNN_NW");
-    return e ? atoi(e) : 0;
-  }();
+  constexpr int force_nw = ECO_AB_NW;
   for (int nw : {16, 8, 4}) {
     if (force_nw && nw != force_nw && nw != 4) continue;
     if (backward && nw == 16) continue;  // the backward's 8-wide weight fragments need > 128 VGPRs
@@ -1180,9 +1188,9 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
   if (!workspace) return fail(ECO_ERR_ARG, "null workspace");
   if ((act_a && !actions_a) || (act_b && !actions_b)) return fail(ECO_ERR_ARG, "act config without actions buffer");
   if ((!q_a && !act_a) || (!q_b && !act_b)) return fail(ECO_ERR_ARG, "nothing to compute (q and act both null)");
-  static const bool no_pair = getenv("ECO_MPNN_NO_PAIR") != nullptr;  // A/B knob: two launches
-  if (no_pair || !(a.xw == 8 && dense_eligible(gs, a.gpb) && a.gpb == 1 && gs->adjbits && !getenv("ECO_MPNN_NO_DENSE") &&
-                   !getenv("ECO_DENSE_V1"))) {
+  const int paths = kernel_paths();
+  if ((paths & (ECO_PATH_NO_PAIR | ECO_PATH_NO_DENSE)) ||
+      !(a.xw == 8 && dense_eligible(gs, a.gpb) && a.gpb == 1 && gs->adjbits)) {
     rc = eco_mpnn_forward(packed_a, n_obs_in, gs, graph_ids, batch, obs_x,
                           reuse_maxdeg ? ECO_NORM_PER_CALL_REUSE : norm_scope, q_a, act_a, actions_a, nullptr,
                           workspace, stream);
@@ -1234,18 +1242,21 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   if (norm_scope == ECO_NORM_PER_CALL && !reuse_maxdeg) {
     call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   }
-  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) {
-    static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernel
-    return v1 ? mpnn_forward_dense_launch(a, saved != nullptr, st) : mpnn_forward_dense2_launch(a, saved != nullptr, st);
+  const int paths = kernel_paths();
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
+#if ECO_AB_DENSE_V1
+    return mpnn_forward_dense_launch(a, saved != nullptr, st);
+#else
+    return mpnn_forward_dense2_launch(a, saved != nullptr, st);
+#endif
   }
-  static const bool no_dl = getenv("ECO_MPNN_NO_DL") != nullptr;  // A/B knob: the CSR-gather kernels
-  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !no_dl && !getenv("ECO_MPNN_NO_DENSE"))
+  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_forward_dl_launch(a, saved != nullptr, workspace, st);
   if (N > MPNN_MAX_SPINS) {  // global-memory embeddings: inference only
     if (saved) return fail(ECO_ERR_ARG, "training forward (saved activations) supports N <= 512");
     // one graph shared by every episode (GSet best-cut search): node-major episode-batched kernels
-    static const bool no_shared = getenv("ECO_MPNN_NO_SHARED") != nullptr;  // A/B knob
-    if (gs->n_graphs == 1 && gs->unit_weights && !no_shared) return mpnn_forward_shared_launch(a, workspace, st);
+    if (gs->n_graphs == 1 && gs->unit_weights && !(paths & ECO_PATH_NO_SHARED))
+      return mpnn_forward_shared_launch(a, workspace, st);
     const int rows_pad = (N + 15) & ~15;
     const size_t lds = (size_t)readout_scratch_floats(rows_pad, 1, 8, true) * sizeof(float);
     (void)hipFuncSetAttribute((const void*)mpnn_forward_large_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1296,12 +1307,16 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.sv = (float*)saved;
   a.dq = dq;
   a.gr = (float*)gradws;
-  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !getenv("ECO_MPNN_NO_DENSE")) {
-    static const bool v1 = getenv("ECO_DENSE_V1") != nullptr;  // A/B knob: the bf16x3 kernels
-    return v1 ? mpnn_backward_dense_launch(a, st) : mpnn_backward_dense2_launch(a, st);
+  const int paths = kernel_paths();
+  if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
+#if ECO_AB_DENSE_V1
+    return mpnn_backward_dense_launch(a, st);
+#else
+    return mpnn_backward_dense2_launch(a, st);
+#endif
   }
-  static const bool no_dl = getenv("ECO_MPNN_NO_DL") != nullptr;
-  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !no_dl && !getenv("ECO_MPNN_NO_DENSE")) return mpnn_backward_dl_launch(a, st);
+  if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
+    return mpnn_backward_dl_launch(a, st);
   const int blocks = (batch + a.gpb - 1) / a.gpb;
   const KCfg k = pick_cfg(a.N, a.gpb, true);
   if (k.lds > LDS_MAX) return fail(ECO_ERR_ARG, "graph block exceeds the LDS budget");

@@ -439,6 +439,9 @@ __device__ __forceinline__ void lin8(f32x4 (&d)[4], const float* W, float xk0, f
   }
 }
 
+#if ECO_AB_DENSE_V1
+// The round-2 bf16x3 kernels, superseded by eco_mpnn_dense2.h (fp16x2).  Compiled only into A/B builds
+// (-DECO_AB_DENSE_V1=1, tools/); the product library has no path to them.
 // LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
 //      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
 //      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
@@ -1025,9 +1028,8 @@ static int mpnn_backward_dense_launch(const MpnnArgs& a, hipStream_t st) {
   if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
   // 16 waves x 1 tile (latency hiding; 2 VGPRs spill) is faster than 8 x 2 (no spills): 0.70 vs 0.82 ms
-  // at M=2048 ER-200.  ECO_MPNN_BWD8 selects the 8 x 2 variant for A/B measurements.
-  static const bool w8 = getenv("ECO_MPNN_BWD8") != nullptr;
-  if (!w8) {
+  // at M=2048 ER-200.
+  if (true) {
     (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel<16, 1>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     mpnn_backward_dense_kernel<16, 1><<<blocks, 1024, lds, st>>>(a);
@@ -1055,5 +1057,7 @@ static int mpnn_forward_dense_launch(const MpnnArgs& a, bool save, hipStream_t s
   }
   return check_launch("mpnn_forward_dense");
 }
+
+#endif  // ECO_AB_DENSE_V1
 
 }  // namespace eco

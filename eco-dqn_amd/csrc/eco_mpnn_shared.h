@@ -752,8 +752,9 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   uint64_t* key = reinterpret_cast<uint64_t*>((char*)workspace + WS_KEY_OFFSET);
   sb.key = key;
-  static const bool no_cache = getenv("ECO_SHARED_NO_CACHE") != nullptr;  // A/B knob: rebuild every call
-  if (no_cache) (void)hipMemsetAsync(key, 0xFF, 2 * sizeof(uint64_t), st);
+#if ECO_AB_SHARED_NO_CACHE  // A/B builds only (tools/): rebuild the tables every call
+  (void)hipMemsetAsync(key, 0xFF, 2 * sizeof(uint64_t), st);
+#endif
   shared_key_kernel<<<1, SK_THREADS, 0, st>>>(a, key);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.nt16 * 4 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);

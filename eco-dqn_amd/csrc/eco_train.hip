@@ -33,6 +33,13 @@ constexpr int MAX_JOBS = 10;
 #define WGRAD_WG_X 3  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
 #endif
 #endif
+// Compile-time A/B variants (tools/ builds only; the product library has exactly one weight-gradient path)
+#ifndef ECO_AB_WGRAD_F32
+#define ECO_AB_WGRAD_F32 0  // wgrad_kernel: the f32-MFMA reduction
+#endif
+#ifndef ECO_AB_WGRAD_FH
+#define ECO_AB_WGRAD_FH 0  // wgrad_fh_kernel: the fp16x2 reduction
+#endif
 #ifndef WGRAD_FH_WG_X
 #define WGRAD_FH_WG_X 3  // wgrad_fh_kernel: workgroups per CU over all jobs (27 KB LDS each)
 #endif
@@ -43,7 +50,9 @@ constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
 constexpr int WROWS = 32;                  // rows per LDS tile
-constexpr int LDY = 68, LDX = 132;         // padded LDS row strides
+#if ECO_AB_WGRAD_F32
+constexpr int LDY = 68, LDX = 132;         // padded LDS row strides (wgrad_kernel)
+#endif
 
 struct WJobs {
   WJob j[MAX_JOBS];
@@ -53,6 +62,7 @@ struct WJobs {
   int first[MAX_JOBS + 1];  // wgrad_bf3_kernel: first flat block of job j (1-D grid of first[n] blocks)
 };
 
+#if ECO_AB_WGRAD_F32
 // One workgroup (4 waves) reduces a contiguous row range of one job: 32-row tiles of dY and
 // X are staged in LDS with 16-byte coalesced loads; each wave owns up to two 32x32 output
 // tiles (o-tile, i-tile) and runs v_mfma_f32_32x32x2_f32 over the rows (k = row pair).
@@ -151,6 +161,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
     }
   }
 }
+
+#endif  // ECO_AB_WGRAD_F32
 
 // Same reduction on 32x32x16 bf16 MFMAs: dY and X are split EXACTLY into three bf16 pieces while a
 // 32-row tile is staged (split3_bits), and the six products above 2^-24 relative are accumulated in
@@ -382,6 +394,7 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   else wgrad_bf3_job<false>(jobs, slabs, jb, sY, sX);
 }
 
+#if ECO_AB_WGRAD_FH
 // Same reduction on fp16x2 operands (eco_mpnn_dense2.h's numerics) and 32x32x16 f16 MFMAs: the 32-row tiles
 // of dY and X are staged in LDS as f32, transposed to [column][row] (stride 36 floats: the 16 lanes of a
 // ds_read_b128 group hit 16 disjoint 4-bank groups) through the same register double buffers.  Each wave
@@ -574,6 +587,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGRAD_FH_WA
     }
   }
 }
+
+#endif  // ECO_AB_WGRAD_FH
 
 // fixed-order sum of the slabs of every job into the flat gradient
 __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad) {
@@ -1007,48 +1022,37 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, xw, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
-  static const bool f32_wgrad = getenv("ECO_WGRAD_F32") != nullptr;  // A/B switch: the f32-MFMA reduction
-  static const bool fh_wgrad = getenv("ECO_WGRAD_FH") != nullptr;    // A/B switch: the fp16x2 reduction
-  // A/B knob: workgroups of each K = 128 job (Wm, Wu); the other jobs share the rest of the resident wave evenly
-  static const int big_wg = [] { const char* e = getenv("ECO_WGRAD_BIG"); return e ? atoi(e) : 0; }();
-  static const bool even_wg = getenv("ECO_WGRAD_EVEN") != nullptr;  // A/B knob: the round-2 even split
-  if (f32_wgrad) {
-    J.nwg = WG_PER_JOB;
-    for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
-    wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
-  } else {
+#if ECO_AB_WGRAD_F32  // A/B builds only (tools/): the f32-MFMA reduction
+  J.nwg = WG_PER_JOB;
+  for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
+  wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
+#else
+  {
     // one resident wave of workgroups over the 256 CUs (46 KB LDS: 3 per CU for bf16x3; 27 KB and 168 VGPRs:
     // 3 per CU for fp16x2).  Measured splits (M = 2048 ER-200): in proportion to the bytes each job reads,
     // 1.28 vs 1.05 ms per gradient step of backward + weight gradients against an even split; more workgroups
-    // for the K = 128 jobs at the others' expense (ECO_WGRAD_BIG = 96 / 112) slower again (9.25 / 12.1 vs 8.66 ms
-    // per vector step): the K <= 64 jobs cost as much per row.  The fp16x2 kernel measured 0.62 vs 0.52 ms per
-    // launch: its per-fragment scales and splits sit after the barrier, on the critical path.
-    const int total = (fh_wgrad ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
-    int nbig = 0;
-    double rows = 0.0, rows_small = 0.0;
-    for (int j = 0; j < n; ++j) {
-      const bool big = J.j[j].K1 + J.j[j].K2 == 128;
-      nbig += big;
-      rows += J.j[j].R;
-      if (!big) rows_small += J.j[j].R;
-    }
+    // for the K = 128 jobs at the others' expense (96 / 112 each) slower again (9.25 / 12.1 vs 8.66 ms
+    // per vector step): the K <= 64 jobs cost as much per row.  The fp16x2 kernel (ECO_AB_WGRAD_FH builds)
+    // measured 0.62 vs 0.52 ms per launch: its per-fragment scales and splits sit after the barrier, on the
+    // critical path.
+    const int total = (ECO_AB_WGRAD_FH ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
+    double rows = 0.0;
+    for (int j = 0; j < n; ++j) rows += J.j[j].R;
     J.first[0] = 0;
     for (int j = 0; j < n; ++j) {
-      const bool big = J.j[j].K1 + J.j[j].K2 == 128;
       // in proportion to the job's rows (a row costs about the same in every job); the per-graph readout job
       // (R = batch) gets one
-      int g = (int)(total * (double)J.j[j].R / rows);
-      if (even_wg) g = total / n;
-      if (big_wg > 0 && nbig > 0 && nbig < n)  // A/B: big_wg for each K = 128 job, the rest by rows
-        g = big ? big_wg : (int)((total - nbig * big_wg) * (double)J.j[j].R / rows_small);
+      const int g = (int)(total * (double)J.j[j].R / rows);
       J.nwgj[j] = std::max(1, std::min(WG_PER_JOB, g));
       J.first[j + 1] = J.first[j] + J.nwgj[j];
     }
-    if (fh_wgrad)
-      wgrad_fh_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
-    else
-      wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
+#if ECO_AB_WGRAD_FH
+    wgrad_fh_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
+#else
+    wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
+#endif
   }
+#endif
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
   ColJobs CJ{};
   CJ.j[0] = ColJob{DWRA, batch, 64, 64, grad + fo.Wr, 1};
@@ -1170,10 +1174,9 @@ extern "C" int eco_replay_compact_sample(const eco_env_config* cfg, const void* 
   const double* tab = (const double*)((const uint8_t*)env_state + L.off_tab + 256);
   const long long P = (long long)capacity + env_batch;
   // threads per transition: 4096 workgroups of a few nodes' work each are latency chains (ring slot -> graph ->
-  // rows -> count -> features); smaller workgroups keep more of them resident.  ECO_SAMPLE_THREADS: A/B knob
-  static const int nt_env = [] { const char* e = getenv("ECO_SAMPLE_THREADS"); return e ? atoi(e) : 0; }();
+  // rows -> count -> features); smaller workgroups keep more of them resident
   // (ER-200 x M = 2048: 30.6 / 24.2 / 21.0 us per call at 256 / 128 / 64 threads, profiles/r03/ab/sample_threads_*)
-  const int nt = (nt_env == 64 || nt_env == 128 || nt_env == 256) ? nt_env : (cfg->n_spins <= 256 ? 64 : 128);
+  const int nt = cfg->n_spins <= 256 ? 64 : 128;
   replay_compact_sample_kernel<<<dim3(2, m), nt, (size_t)cfg->n_spins * 4, (hipStream_t)stream>>>(
       *cfg, compact_carve(const_cast<void*>(ring), cfg->n_spins, P), P, capacity, size, pushed, m,
       rng3(seed, counter, 0x5A5A), tab, *gs, xs, xn, graph_ids, actions, rewards, dones);

@@ -32,6 +32,8 @@ ECO_MAX_SPINS = 2048
 ECO_COMPACT_MAX_SPINS = 8192  # include/eco_hip.h: compact replay (sample rebuilds s' in LDS)
 ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL, ECO_NORM_PER_CALL_REUSE = 0, 1, 2
 ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
+# kernel-path policy bits (eco_set_kernel_paths)
+ECO_PATH_NO_DENSE, ECO_PATH_NO_DL, ECO_PATH_NO_SHARED, ECO_PATH_NO_PAIR = 1, 2, 4, 8
 
 
 class EnvConfig(ctypes.Structure):
@@ -79,6 +81,7 @@ _SIG = {
                                     _P, _P]),
     "eco_env_read": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P, _P, _P]),
     "eco_check_errors": (ctypes.c_int, [_P]),
+    "eco_set_kernel_paths": (_I, [_I]),
     "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), ctypes.POINTER(GraphSet), _P, _I, _P,
                                               _P]),
     "eco_mpnn_param_count": (ctypes.c_size_t, [_I]),
@@ -165,3 +168,19 @@ def stream_ptr(stream=None):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+class kernel_paths:
+    """Context manager routing MPNN calls to another product kernel family (eco_set_kernel_paths, ECO_PATH_*
+    bits) and restoring the previous policy on exit: `with kernel_paths(ECO_PATH_NO_DENSE): ...`."""
+
+    def __init__(self, mask):
+        self.mask = int(mask)
+
+    def __enter__(self):
+        self.prev = lib.eco_set_kernel_paths(self.mask)
+        return self
+
+    def __exit__(self, *exc):
+        lib.eco_set_kernel_paths(self.prev)
+        return False

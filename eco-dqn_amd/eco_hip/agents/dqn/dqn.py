@@ -290,7 +290,12 @@ class DQN:
         pushes since its last episode ended), reused otherwise (warned once)."""
         k = self.B if episodes is None else int(episodes.sum())
         if self.regenerate_graphs is None:
-            return self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), k)]
+            ids = self.graph_pool_ids[self._rng.integers(0, len(self.graph_pool_ids), k)]
+            if episodes is None:
+                return ids
+            out = np.zeros(self.B, np.int64)   # VecSpinSystem.reset reads graph_ids[mask]: B-long
+            out[episodes] = ids
+            return out
         kind, param = self.regenerate_graphs[:2]
         weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
         n_slots = len(self._slot_users)
@@ -358,6 +363,8 @@ class DQN:
             self._loss_buf = torch.zeros(4096, dtype=torch.float32, device=self.device)
             self._loss_t = np.zeros(4096, np.int64)
             self._loss_n = 0
+        # the reference's `losses` list is local to one learn() call (dqn.py:269): report from here on
+        self._loss_start = self._loss_n
         # every episode ends exactly at max_steps only for reversible spins with Stopping.NORMAL
         # (spinsystem.py:539-554); otherwise dones are read back after each vector step
         self._lockstep = self.env.reversible_spins and self.env.cfg.stopping == 1
@@ -431,7 +438,12 @@ class DQN:
                 on_vector_step(t)
             if not self._ready:
                 continue
-            if self.evaluate and t // self.test_frequency > t_prev // self.test_frequency:
+            crossed_test = t // self.test_frequency > t_prev // self.test_frequency
+            if crossed_test and self.regenerate_graphs is not None:
+                # graphs regenerated with check=False since the last sync point: an edge-slot overflow
+                # sets the device error word (the slot becomes an empty graph); surface it here
+                self.graphs.check_errors()
+            if self.evaluate and crossed_test:
                 tk = (t // self.test_frequency) * self.test_frequency
                 test_score, test_solution = self.evaluate_agent()
                 if verbose and rank == 0:
@@ -446,6 +458,8 @@ class DQN:
                 tk = (t // self.save_network_frequency) * self.save_network_frequency
                 main, ext = os.path.splitext(self.network_save_path)
                 self.save(main + str(tk) + (ext or ".pth"))
+        if self.regenerate_graphs is not None:
+            self.graphs.check_errors()
         losses = self.losses()
         if rank == 0 and self.test_save_path is not None:
             path = self.test_save_path
@@ -462,12 +476,14 @@ class DQN:
         return losses[-100:]
 
     def losses(self):
-        """[[timestep, loss], ...] of every gradient step so far (dqn.py:339, one host copy)."""
+        """[[timestep, loss], ...] of every gradient step of the current (or last) learn() call
+        (dqn.py:269,339; one host copy)."""
         n = getattr(self, "_loss_n", 0)
-        if n == 0:
+        s = getattr(self, "_loss_start", 0)
+        if n <= s:
             return []
-        vals = self._loss_buf[:n].cpu().tolist()
-        return [[int(t), v] for t, v in zip(self._loss_t[:n], vals)]
+        vals = self._loss_buf[s:n].cpu().tolist()
+        return [[int(t), v] for t, v in zip(self._loss_t[s:n], vals)]
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()

@@ -240,6 +240,17 @@ int eco_mpnn_forward_pair(const float *packed_a, const float *packed_b, int32_t 
                           float *q_a, const eco_act_config *act_a, int32_t *actions_a, float *q_b,
                           const eco_act_config *act_b, int32_t *actions_b, void *workspace, eco_stream_t stream);
 
+/* Kernel-path policy of the MPNN dispatcher (process-wide, default 0 = the fastest kernel for each shape).
+ * Each bit routes the calls it names to another product kernel family that also serves other shapes, with
+ * the same results within the fp32 bars of the tests (tests/test_kernel_paths_gpu.py runs every bit):
+ *   NO_DENSE  -- blocks the dense-aggregation kernels would take run the CSR-gather kernels instead;
+ *   NO_DL     -- one-graph blocks of 224 < N <= 512 run the CSR-gather kernels;
+ *   NO_SHARED -- N > 512 single-graph inference runs the per-episode global-memory kernel;
+ *   NO_PAIR   -- eco_mpnn_forward_pair runs as two eco_mpnn_forward calls.
+ * The library reads no environment variables; this call is the only switch. Returns the previous mask. */
+enum { ECO_PATH_NO_DENSE = 1, ECO_PATH_NO_DL = 2, ECO_PATH_NO_SHARED = 4, ECO_PATH_NO_PAIR = 8 };
+int32_t eco_set_kernel_paths(int32_t mask);
+
 /* ---- DQN train step (dqn.py:403-451) ---- */
 
 size_t eco_mpnn_backward_workspace_bytes(int32_t n_spins, int32_t batch);

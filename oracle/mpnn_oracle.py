@@ -87,36 +87,64 @@ def forward(w, obs, n_obs_in=7, norm_max=None):
     return q.squeeze()
 
 
+def batch_norm_max(states, n_obs_in=7):
+    """norm.max() of mpnn.py:102 for a whole batch of observations [B, n_obs_in+N, N]: the largest
+    clamped nonzero count of an adjacency row (:36-37)."""
+    return (states[:, n_obs_in:, :] != 0).sum(dim=2).clamp_min(1).max()
+
+
+def forward_chunked(w, states, n_obs_in=7, chunk=None):
+    """forward() of a batch evaluated `chunk` graphs at a time with the batch's own norm.max() (so the
+    result is the whole batch's forward: the [k, N, N, 63] edge tensor of :90-100 stays bounded)."""
+    if chunk is None or states.shape[0] <= chunk:
+        return forward(w, states, n_obs_in).reshape(states.shape[0], -1)
+    nmax = batch_norm_max(states, n_obs_in)
+    return torch.cat([forward(w, states[i:i + chunk], n_obs_in, norm_max=nmax).reshape(-1, states.shape[-1])
+                      for i in range(0, states.shape[0], chunk)])
+
+
 def train_step(w, adam_state, states, actions, rewards, states_next, dones,
                gamma=0.95, lr=1e-4, eps=1e-8, target_w=None, double_dqn=True, n_obs_in=7,
-               reversible=True, allowed_value=-1.0):
+               reversible=True, allowed_value=-1.0, chunk=None):
     """dqn.py:403-451.  Reversible env: gather/argmax over all N actions (:408-415).  Irreversible
     (S2V) env: actions whose spin row differs from the allowed action state are masked to -10000
     before the argmax / max (:417-428); a terminal s' (every action masked) gives argmax 0, and its
     (1 - done) factor zeroes the term.  `adam_state` = dict(step=int, m={k: tensor}, v={k: tensor});
-    torch.optim.Adam semantics (bias-corrected, eps added to sqrt(v_hat)).  Returns (new_w, loss)."""
+    torch.optim.Adam semantics (bias-corrected, eps added to sqrt(v_hat)).  Returns (new_w, loss).
+    chunk: evaluate the forwards and the loss gradient `chunk` graphs at a time (batch-global norm.max(),
+    gradients accumulated over the chunks of the mean loss) to bound the oracle's memory."""
     target_w = w if target_w is None else target_w
     B = states_next.shape[0]
     with torch.no_grad():
         if reversible:
             if double_dqn:
-                a_star = forward(w, states_next, n_obs_in).reshape(B, -1).argmax(1, True)
-                q_t = forward(target_w, states_next, n_obs_in).reshape(B, -1).gather(1, a_star)
+                a_star = forward_chunked(w, states_next, n_obs_in, chunk).argmax(1, True)
+                q_t = forward_chunked(target_w, states_next, n_obs_in, chunk).gather(1, a_star)
             else:
-                q_t = forward(target_w, states_next, n_obs_in).reshape(B, -1).max(1, True)[0]
+                q_t = forward_chunked(target_w, states_next, n_obs_in, chunk).max(1, True)[0]
         else:
-            target_preds = forward(target_w, states_next, n_obs_in).reshape(B, -1)
+            target_preds = forward_chunked(target_w, states_next, n_obs_in, chunk)
             disallowed = states_next[:, 0, :] != allowed_value
             if double_dqn:
-                preds = forward(w, states_next, n_obs_in).reshape(B, -1).masked_fill(disallowed, -10000)
+                preds = forward_chunked(w, states_next, n_obs_in, chunk).masked_fill(disallowed, -10000)
                 q_t = target_preds.gather(1, preds.argmax(1, True))
             else:
                 q_t = target_preds.masked_fill(disallowed, -10000).max(1, True)[0]
     td = rewards + (1 - dones) * gamma * q_t
     wg = {k: v.clone().requires_grad_(True) for k, v in w.items()}
-    q = forward(wg, states, n_obs_in).reshape(states.shape[0], -1).gather(1, actions)
-    loss = F.mse_loss(q, td, reduction="mean")
-    loss.backward()
+    if chunk is None or states.shape[0] <= chunk:
+        q = forward(wg, states, n_obs_in).reshape(states.shape[0], -1).gather(1, actions)
+        loss = F.mse_loss(q, td, reduction="mean")
+        loss.backward()
+    else:  # mean over B of the squared errors, one chunk's sum at a time
+        nmax = batch_norm_max(states, n_obs_in)
+        total = 0.0
+        for i in range(0, B, chunk):
+            q = forward(wg, states[i:i + chunk], n_obs_in, norm_max=nmax).reshape(-1, states.shape[-1])
+            part = ((q.gather(1, actions[i:i + chunk]) - td[i:i + chunk]) ** 2).sum() / B
+            part.backward()
+            total += part.item()
+        loss = torch.tensor(total)
     adam_state["grad"] = {k: wg[k].grad.detach().clone() for k in KEYS}  # loss.backward() result
     adam_state["step"] += 1
     t = adam_state["step"]

@@ -37,6 +37,16 @@ def test_pure_queries_without_gpu():
     assert _lib.lib.eco_env_state_bytes(ctypes.byref(cfg), 8192) > 8192 * 200 * 8
 
 
+def test_set_kernel_paths_returns_previous_and_masks_unknown_bits():
+    """eco_set_kernel_paths is host-only: the policy word the MPNN dispatcher reads (no GPU needed)."""
+    from eco_hip import _lib
+    prev = _lib.lib.eco_set_kernel_paths(0xFF)
+    assert _lib.lib.eco_set_kernel_paths(prev) == 0xF
+    with _lib.kernel_paths(_lib.ECO_PATH_NO_PAIR):
+        assert _lib.lib.eco_set_kernel_paths(_lib.ECO_PATH_NO_PAIR) == _lib.ECO_PATH_NO_PAIR
+    assert _lib.lib.eco_set_kernel_paths(prev) == prev
+
+
 def test_boundary_errors_map_to_reference_exceptions():
     import pytest
     from eco_hip.envs.batched import make_config

@@ -1,7 +1,7 @@
 """The dense-aggregation MPNN kernels (eco_mpnn_dense.h: blocks of <= 224 rows, +-1 weights) against
 the CSR-gather kernels (eco_mpnn.hip) on the same inputs, and against the fp32 torch oracle.
 
-The CSR path is selected per call with ECO_MPNN_NO_DENSE=1.  Both compute the reference's fp32
+The CSR path is selected per call with the ECO_PATH_NO_DENSE kernel-path bit (eco_set_kernel_paths).  Both compute the reference's fp32
 arithmetic in a different summation order (dense: exact bf16x3 splits, fp32 accumulation), so the bars
 are the oracle tolerances of test_mpnn_gpu / test_dqn_gpu:
   Q: |q - q_ref| <= 5e-5 (1 + |q_ref|);  gradients: relative L2 error < 2e-4 per parameter tensor against
@@ -11,7 +11,6 @@ in-kernel (adjbits dropped), several graphs per block (N = 20, 64), padding rows
 non-unit weights; and the dense kernels for one graph of 224 < N <= 512 per workgroup (eco_mpnn_dl.h: BA-500,
 N = 512 without padding, 497 with a padded last tile, 300 / 225 with waves of unequal tile counts), whose
 gradients are checked against float64 autograd of the oracle on the GPU."""
-import os
 
 import numpy as np
 import pytest
@@ -37,11 +36,8 @@ def _inputs(n, B, seed, kind="ER", param=0.15):
 def _run(net, store, x, dq, scope, dense):
     from eco_hip.networks.mpnn import MPNN
     B, n = x.shape[0], x.shape[1]
-    if dense:
-        os.environ.pop("ECO_MPNN_NO_DENSE", None)
-    else:
-        os.environ["ECO_MPNN_NO_DENSE"] = "1"
-    try:
+    from eco_hip import _lib
+    with _lib.kernel_paths(0 if dense else _lib.ECO_PATH_NO_DENSE):
         gids = torch.arange(B, dtype=torch.int32, device="cuda")
         q = net.forward_graphs(x, store, gids, norm_scope=scope).clone()
         saved = torch.empty(MPNN.saved_bytes(n, B), dtype=torch.uint8, device="cuda")
@@ -50,8 +46,6 @@ def _run(net, store, x, dq, scope, dense):
         net.backward_graphs(x, store, gids, saved, dq, grad)
         torch.cuda.synchronize()
         return q.cpu(), qs.cpu(), grad.cpu()
-    finally:
-        os.environ.pop("ECO_MPNN_NO_DENSE", None)
 
 
 def _scaled_err(a, b):

@@ -353,18 +353,21 @@ def test_learn_evaluates_saves_and_pickles(tmp_path):
     assert list(sd) == mo.KEYS
 
 
-@pytest.mark.parametrize("n,B,basis", [(20, 64, "SIGNED"), (200, 16, "BINARY")])
-def test_compact_replay_matches_feature_replay(n, B, basis):
+@pytest.mark.parametrize("n,B,basis,kind", [(20, 64, "SIGNED", "ER"), (200, 16, "BINARY", "ER"),
+                                            (257, 12, "SIGNED", "ER"), (500, 8, "SIGNED", "BA")])
+def test_compact_replay_matches_feature_replay(n, B, basis, kind):
     """The compact replay (integer env state per transition, features rebuilt on sample) returns exactly
     the transitions the fp32 feature ring returns for the same pushes and the same sampling keys: node
     features bitwise, actions, rewards, dones, graph ids -- across a masked reset (new s rows) and a
-    ring wrap.  The compact ring stores one state per transition: 4N + 80 B against 64N B (<= 1 KB at N=200)."""
+    ring wrap.  The compact ring stores one state per transition: 4N + 80 B against 64N B (<= 1 KB at N=200).
+    N = 257 and BA-500 (configs[3]) take the sample kernel's 128-thread path for N > 256 (several vertices per
+    thread, csrc/eco_train.hip replay_compact_sample)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
                                     SpinBasis)
     from eco_hip.agents.dqn.utils import ReplayBuffer, CompactReplayBuffer
-    store = GraphStore.random("ER", 2 * B, n, 0.15, seed=n)
+    store = GraphStore.random(kind, 2 * B, n, 0.15 if kind == "ER" else 4, seed=n)
     env = VecSpinSystem(store, B, 2 * n, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
                         spin_basis=SpinBasis[basis], norm_rewards=True, basin_reward=1. / n)
@@ -455,3 +458,55 @@ def test_regenerate_graphs_with_replay_longer_than_an_episode_batch():
     assert np.array_equal(np.sort(seen[4][0]), np.sort(seen[0][0]))
     assert seen[4][2] - seen[1][2] >= C
     assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()
+
+
+def test_learn_with_staggered_dones_resets_only_finished_episodes():
+    """with Stopping.EARLY (spinsystem.py:541-556, done after 15 steps without a new best)
+    episodes finish at different steps, so learn() takes the partial-reset path of iteration() (dqn.py:306-327
+    resets each finished env on its own) without regenerate_graphs.  Every reset episode gets a pool graph,
+    the live ones keep theirs, and training proceeds; a second learn() reports only its own losses
+    (the reference's `losses` list is local to learn(), dqn.py:269)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis, Stopping)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN
+    n, B = 20, 64
+    pool = np.arange(100, 228)
+    store = GraphStore.random("ER", 256, n, 0.15, seed=12)
+    env = VecSpinSystem(store, B, 2 * n, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n,
+                        stopping=Stopping.EARLY)
+    agent = DQN(env, lambda: MPNN(device="cuda"), init_weight_std=0.01, replay_start_size=4 * B,
+                replay_buffer_size=4096, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
+                initial_learning_rate=1e-4, peak_learning_rate=1e-4, final_learning_rate=1e-4, update_frequency=32,
+                minibatch_size=64, final_exploration_rate=0.05, final_exploration_step=20000, seed=21,
+                evaluate=False, test_save_path=None, graph_pool_ids=pool)
+    assert not agent._lockstep
+    hist = {"partial": 0}
+    prev = {}
+
+    def watch(t):
+        gids = agent.env.graph_ids.cpu().numpy()
+        steps = agent.env.read()["current_step"].cpu().numpy()
+        assert np.isin(gids, pool).all()
+        if "steps" in prev:
+            reset = steps == 0
+            if reset.any() and not reset.all():
+                hist["partial"] += 1
+                # episodes that were not reset kept their graph and advanced by one step
+                keep = ~reset
+                np.testing.assert_array_equal(gids[keep], prev["gids"][keep])
+                np.testing.assert_array_equal(steps[keep], prev["steps"][keep] + 1)
+        prev["gids"], prev["steps"] = gids, steps
+
+    first = agent.learn(timesteps=B * 60, on_vector_step=watch)
+    assert hist["partial"] > 0, "no staggered resets happened"
+    assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()
+    n1 = len(agent.losses())
+    assert n1 == agent.grad_steps and len(first) == min(100, n1)
+    agent.learn(timesteps=B * 20)
+    second = agent.losses()
+    assert len(second) == agent.grad_steps - n1 > 0

@@ -167,3 +167,24 @@ def test_oracle_norm_max_chunking():
     parts = torch.cat([mo.forward(w, obs[i:i + 1], norm_max=nmax).reshape(1, -1) for i in range(4)])
     torch.testing.assert_close(parts, full, rtol=0, atol=1e-6)
     assert not torch.allclose(mo.forward(w, obs[0]), full[0], atol=1e-6)  # the coupling is real
+
+
+def test_oracle_chunked_train_step_matches_whole_batch():
+    """train_step(chunk=k) (used at the BA-500 M = 256 size, where the [B, N, N, 63] edge tensor of one call
+    would not fit) equals the one-call train step on the reference's own fixture: same loss, gradients and
+    Adam step within fp32 summation-order noise."""
+    f = np.load(os.path.join(GOLDEN, "dqn_step.npz"))
+    w = _weights(f, "w0/")
+    tw = _weights(f, "target/")
+    p = "s0/"
+    args = (torch.from_numpy(f[p + "states"]).float(), torch.from_numpy(f[p + "actions"]),
+            torch.from_numpy(f[p + "rewards"]), torch.from_numpy(f[p + "states_next"]).float(),
+            torch.from_numpy(f[p + "dones"]))
+    s1, s2 = {"step": 0, "m": {}, "v": {}}, {"step": 0, "m": {}, "v": {}}
+    w1, l1 = mo.train_step(w, s1, *args, target_w=tw)
+    w2, l2 = mo.train_step(w, s2, *args, target_w=tw, chunk=3)
+    assert args[0].shape[0] > 3 and args[0].shape[0] % 3 != 0
+    assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l1))
+    for k in mo.KEYS:
+        torch.testing.assert_close(s2["grad"][k], s1["grad"][k], rtol=1e-4, atol=1e-7)
+        torch.testing.assert_close(w2[k], w1[k], rtol=1e-5, atol=2e-7)

@@ -224,6 +224,66 @@ def test_learn_er200_first_train_step_matches_oracle():
         assert float((d > 2e-6).float().mean()) <= 0.01, k
 
 
+def test_learn_ba500_first_train_step_matches_oracle():
+    """configs[3]'s training path at N = 500 (BA m=4, +-1 weights): DQN.learn() with the compact replay (its
+    sample kernel's N > 256 path rebuilds s and s' of 500 vertices), the double-DQN s' pair and training
+    forward through the one-graph-per-workgroup dense kernels (eco_mpnn_dl.h), the backward and the
+    weight-gradient reduction; the first train_step against oracle.train_step on the same sampled minibatch
+    (evaluated 16 graphs at a time with the batch's norm.max()).  Bars as the ER-200 test above."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN
+    n, B, M = 500, 256, 256
+    store = GraphStore.random("BA", B, n, 4, seed=55)
+    env = VecSpinSystem(store, B, 2 * n, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
+    agent = DQN(env, lambda: MPNN(device="cuda"), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
+                replay_start_size=2 * B, replay_buffer_size=B * 8, gamma=0.95, update_target_frequency=4000,
+                update_learning_rate=False, initial_learning_rate=1e-4, peak_learning_rate=1e-4,
+                final_learning_rate=1e-4, update_frequency=32, minibatch_size=64, train_minibatch=M,
+                initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
+                adam_epsilon=1e-8, seed=13, evaluate=False, test_save_path=None)
+    assert agent.compact_replay
+    with torch.no_grad():
+        agent.target_network.flat.add_(torch.randn(agent.target_network.flat.shape, device="cuda",
+                                                   generator=torch.Generator(device="cuda").manual_seed(2)) * 0.01)
+    rec = {}
+    orig = agent.train_step
+
+    def spy(tr, sync_loss=True, loss_out=None):
+        if not rec:
+            rec["tr"] = [t.clone() for t in tr]
+            rec["w"] = _flat_to_dict(agent.network.flat.clone())
+            rec["tw"] = _flat_to_dict(agent.target_network.flat.clone())
+            loss = orig(tr, sync_loss=True, loss_out=loss_out)
+            rec["loss"] = loss
+            rec["grad"] = _flat_to_dict(agent.grad.clone())
+            rec["w1"] = _flat_to_dict(agent.network.flat.clone())
+            return torch.tensor([loss], device="cuda")
+        return orig(tr, sync_loss=sync_loss, loss_out=loss_out)
+
+    agent.train_step = spy
+    agent.learn(timesteps=B * 3)
+    assert rec, "learn() never trained"
+    xs, act, rew, xn, done, gid = rec["tr"]
+    assert xs.shape[0] == M
+    adj = dense_batch(store, gid)
+    st = {"step": 0, "m": {}, "v": {}}
+    w1, loss = mo.train_step(rec["w"], st, _obs(xs, adj), act.long().unsqueeze(1), rew.unsqueeze(1),
+                             _obs(xn, adj), done.unsqueeze(1), gamma=0.95, lr=1e-4, eps=1e-8,
+                             target_w=rec["tw"], chunk=16)
+    assert abs(rec["loss"] - loss) <= 1e-4 * abs(loss), (rec["loss"], loss)
+    for k in mo.KEYS:
+        assert _rel(rec["grad"][k], st["grad"][k]) < 2e-4, k
+        d = (rec["w1"][k] - w1[k]).abs()
+        assert float(d.max()) <= 2e-4 + 1e-6, k
+        assert float((d > 2e-6).float().mean()) <= 0.01, k
+
+
 @pytest.mark.parametrize("episodes", [1, 4])
 def test_large_forward_n2000_matches_oracle(episodes):
     from eco_hip.graphs import GraphStore
