@@ -448,6 +448,39 @@ def process_group_info(world, per_rank_s, steps, local, device):
             "ms_per_step_min": min(ms), "ms_per_step_max": max(ms)}
 
 
+def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=1.0,
+                      n_graphs=None):
+    """The benched configs[2] / configs[3] agent: B episodes on a pool of B seeded graphs (one per episode),
+    experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377) batched, with the large-batch recipe of
+    tests/test_training_quality_gpu.py (target sync every update_target_frequency / update_frequency gradient
+    steps, lr 1e-4 x sqrt(M / 64)) and a replay ring of `replay_episodes` x B x T transitions: the B lockstep
+    episodes push B per vector step, so a ring of one episode's worth holds every time step of the episodes
+    (the reference's 15,000 transitions span ~19 whole ER-200 episodes); B x 16 (round 3) held only the last 16
+    steps and measured 0.935 of the pretrained network's single-attempt cut against 0.974-0.991 with B x T
+    (profiles/r04/quality/).  tests/test_training_quality_er200_gpu.py trains this exact agent.
+    n_graphs: size of the graph pool episodes draw from at each reset (default B).  Returns (agent, store, env, lr)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN
+    T = 2 * n
+    store = GraphStore.random(graph, n_graphs or B, n, gparam, seed=seed, device=dev)
+    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
+    lr = 1e-4 * (minibatch / 64.0) ** 0.5
+    cap = int(B * T * replay_episodes)
+    agent = DQN(env, lambda: MPNN(device=dev), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
+                replay_start_size=3000, replay_buffer_size=cap, gamma=0.95, update_target_frequency=4000,
+                update_learning_rate=False, initial_learning_rate=lr, peak_learning_rate=lr,
+                final_learning_rate=lr, update_frequency=32, minibatch_size=64, train_minibatch=minibatch,
+                initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
+                adam_epsilon=1e-8, seed=seed, target_sync="grad_steps")
+    return agent, store, env, lr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -495,33 +528,13 @@ def main():
     if args.workload == "envstep":
         return envstep_bench(args, world, rank, local, dev, dist)
 
-    from eco_hip.graphs import GraphStore
-    from eco_hip.envs.batched import VecSpinSystem
-    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
-                                    SpinBasis)
-    from eco_hip.networks.mpnn import MPNN
-    from eco_hip.agents.dqn.dqn import DQN
-
     B, n = args.envs, args.n
     T = 2 * n
     seed = 1234 + rank
     gparam = args.param if args.param is not None else (0.15 if args.graph == "ER" else 4)
-    store = GraphStore.random(args.graph, B, n, gparam, seed=seed, device=dev)
+    agent, store, env, lr = build_train_agent(dev, B, n, args.graph, gparam, args.minibatch, seed)
     nnz = np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1)
     gflops = np.array([mpnn_flops(z, n) for z in nnz])
-    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
-                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
-                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
-    # experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377), batched, with the large-batch recipe of
-    # tests/test_training_quality_gpu.py: target sync every update_target_frequency / update_frequency gradient
-    # steps and lr 1e-4 x sqrt(M / 64)
-    lr = 1e-4 * (args.minibatch / 64.0) ** 0.5
-    agent = DQN(env, lambda: MPNN(device=dev), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
-                replay_start_size=3000, replay_buffer_size=B * 16, gamma=0.95, update_target_frequency=4000,
-                update_learning_rate=False, initial_learning_rate=lr, peak_learning_rate=lr,
-                final_learning_rate=lr, update_frequency=32, minibatch_size=64, train_minibatch=args.minibatch,
-                initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
-                adam_epsilon=1e-8, seed=seed, target_sync="grad_steps")
     agent.start()
     train = args.workload == "train"
 

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ... import _lib
-from ...parallel import allreduce_gradients, broadcast_parameters
+from ...parallel import allreduce_gradients_async, broadcast_parameters
 from .utils import CompactReplayBuffer, ReplayBuffer, TestMetric, set_global_seed
 
 
@@ -239,10 +239,12 @@ class DQN:
         return out
 
     # ----------------------------------------------------------------- train
-    def train_step(self, transitions, sync_loss=True, loss_out=None):
+    def train_step(self, transitions, sync_loss=True, loss_out=None, overlap=None):
         """dqn.py:403-451.  transitions = (states_x, actions, rewards, states_next_x, dones, graph_ids)
         as returned by ReplayBuffer.sample.  Returns the loss: a float if sync_loss, else the one-element
-        device tensor it was written to (`loss_out`, or a copy of the agent's loss slot)."""
+        device tensor it was written to (`loss_out`, or a copy of the agent's loss slot).
+        overlap: optional callable issued while the gradient all-reduce is in flight (multi-GPU): work that does
+        not read the gradient or the online weights, e.g. the next minibatch's replay sample."""
         xs, act, rew, xn, done, gid = transitions
         loss_dev = self.loss_dev if loss_out is None else loss_out
         m = xs.shape[0]
@@ -266,7 +268,13 @@ class DQN:
                                        ctypes.c_float(self.gamma), int(bool(self.clip_Q_targets)), _lib.ptr(self.dq),
                                        _lib.ptr(self.sqerr), _lib.ptr(loss_dev), _lib.stream_ptr()))
         net.backward_graphs(xs, self.graphs, gid, self.saved, self.dq, self.grad, workspace=self.bw_ws)
-        scale = allreduce_gradients(self.grad)  # RCCL sum over xGMI (233.7 KB), mean folded into Adam
+        # RCCL sum over xGMI (233.7 KB) on the collective's stream, the mean folded into Adam; independent work
+        # (the caller's `overlap`) is issued on this stream meanwhile
+        work, scale = allreduce_gradients_async(self.grad)
+        if overlap is not None:
+            overlap()
+        if work is not None:
+            work.wait()
         self.adam_step += 1
         _lib.check(_lib.lib.eco_adam(_lib.ptr(net.flat), _lib.ptr(self.grad), _lib.ptr(self.exp_avg),
                                      _lib.ptr(self.exp_avg_sq), net.flat.numel(), self.lr, 0.9, 0.999,
@@ -399,9 +407,17 @@ class DQN:
                 mask = done.cpu().numpy()
                 self._reset_env(self._take_graph_slots(mask), self.seed + self._timestep, mask=done)
         if self._ready:
-            for _ in range(self._k_per_vec):
-                self._last_loss = self.train_step(self.replay_buffer.sample(self.M), sync_loss=False,
-                                                  loss_out=self._loss_slot(self._timestep))
+            # gradient step k's all-reduce overlaps step k+1's replay sample (stream order: the sample rewrites
+            # the minibatch buffers after step k's forwards and backward have read them)
+            nxt = [self.replay_buffer.sample(self.M)]
+            for k in range(self._k_per_vec):
+                tr = nxt.pop()
+                more = k + 1 < self._k_per_vec
+
+                def prefetch():
+                    nxt.append(self.replay_buffer.sample(self.M))
+                self._last_loss = self.train_step(tr, sync_loss=False, loss_out=self._loss_slot(self._timestep),
+                                                  overlap=prefetch if more else None)
                 if (self.grad_steps % self.target_sync_grad_steps == 0 if self.target_sync == "grad_steps"
                         else self._samples_since_sync >= self.target_sync_samples):
                     self.sync_target()
@@ -524,6 +540,8 @@ class DQN:
         act_cfg = self._act_config(0.0)
         act_cfg.reversible = int(env.reversible_spins)
         act_cfg.allowed_value = float(env.allowed_action_value())
+        if self.test_episodes <= slots and env.reversible_spins and env.cfg.stopping == 1:
+            return self._evaluate_one_fill(env, act_cfg, metric)
         while len(scores) < self.test_episodes:
             free = (~active[:slots]).nonzero().flatten().cpu().numpy()
             take = free[:max(0, self.test_episodes - started)]
@@ -569,6 +587,53 @@ class DQN:
             print("\n{}/{} graphs solved optimally".format(np.count_nonzero(np.array(scores) == 0),
                                                           self.test_episodes), end="")
         self.last_evaluation = (scores, solutions)  # per episode, in completion order
+        return float(np.mean(scores)), float(np.mean(solutions))
+
+    def _evaluate_one_fill(self, env, act_cfg, metric):
+        """evaluate_agent when every test episode fits the slots at once (the reference's 50 ER-200 test graphs
+        in 64 slots) and every episode ends exactly at max_steps (reversible spins, Stopping.NORMAL,
+        spinsystem.py:539-554): the same resets, predictions and steps as the refill loop, with no host
+        synchronisation per step.  The k episodes take slots 0..k-1, so each prediction's batch (its norm.max()
+        coupling, dqn.py:546-547) is the contiguous prefix obs_x[:k] -- all of them are active until the last
+        step, as in the refill loop -- and the env is read once at the end.  Scores are listed in completion
+        order (end step, then slot), as the refill loop appends them."""
+        dev = self.device
+        k = self.test_episodes
+        n_graphs = env.graphs.n_graphs
+        mask = np.zeros(env.n_envs, dtype=np.uint8)
+        mask[:k] = 1
+        gids = np.zeros(env.n_envs, dtype=np.int64)
+        gids[:k] = (env._eval_next_graph + np.arange(k)) % n_graphs
+        env._eval_next_graph = (env._eval_next_graph + k) % n_graphs
+        env.reset(graph_ids=gids, mask=mask, seed=self.seed)
+        cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
+        acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
+        sub = acts[:k]
+        act_cfg.counter = 0
+        for _ in range(env.max_steps):
+            self.network.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=_lib.ECO_NORM_PER_CALL,
+                                        act=act_cfg, actions_out=sub)
+            _, rew, _ = env.step(acts)
+            cum += rew
+        st = env.read()
+        ends = st["current_step"][:k].cpu().numpy()
+        order = np.lexsort((np.arange(k), ends))
+        scores, solutions = [], []
+        for i in order.tolist():
+            if metric == TestMetric.BEST:
+                sc, so = float(st["best_score"][i]), float(st["best_solution"][i])
+            elif metric == TestMetric.FINAL:
+                sc, so = float(st["score"][i]), self._final_solution(env, st, i)
+            elif metric == TestMetric.CUMULATIVE_REWARD:
+                sc, so = float(cum[i]), 0.0
+            else:
+                sc, so = 0.0, 0.0
+            scores.append(sc)
+            solutions.append(so)
+        if metric == TestMetric.ENERGY_ERROR:
+            print("\n{}/{} graphs solved optimally".format(np.count_nonzero(np.array(scores) == 0),
+                                                          self.test_episodes), end="")
+        self.last_evaluation = (scores, solutions)
         return float(np.mean(scores)), float(np.mean(solutions))
 
     @staticmethod

@@ -33,6 +33,19 @@ def allreduce_gradients(grad, group=None):
     return 1.0 / world
 
 
+def allreduce_gradients_async(grad, group=None):
+    """Start the sum all-reduce of the flat gradient (RCCL on its own stream) and return (work, scale): the
+    caller issues independent work (the next minibatch's replay sample) and calls work.wait() -- which makes
+    the current stream wait for the collective -- before the optimiser reads grad.  work is None without a
+    process group (or at world size 1)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None, 1.0
+    world = dist.get_world_size(group)
+    if world == 1:
+        return None, 1.0
+    return dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group, async_op=True), 1.0 / world
+
+
 def broadcast_parameters(flat, src=0, group=None):
     """Make every rank start from rank src's parameters (DQN init)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:

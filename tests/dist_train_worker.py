@@ -47,28 +47,30 @@ def main():
     all0 = [torch.zeros_like(w0) for _ in range(world)]
     dist.all_gather(all0, w0)
     import eco_hip.agents.dqn.dqn as dqn_mod
-    real_allreduce = dqn_mod.allreduce_gradients
+    real_allreduce = dqn_mod.allreduce_gradients_async
     rec = {"checked": 0, "m_err": 0.0}
 
     def spy_allreduce(grad, group=None):
         locals_ = [torch.zeros_like(grad) for _ in range(world)]
         dist.all_gather(locals_, grad)                         # every rank's local gradient, rank order
-        scale = real_allreduce(grad, group)
+        work, scale = real_allreduce(grad, group)
+        assert work is not None, "no collective was started"
+        work.wait()
         total = locals_[0].clone()
         for g in locals_[1:]:
             total += g
         assert torch.equal(grad, total), "all-reduced gradient != rank-order sum of the local gradients"
         assert scale == 1.0 / world, scale
         rec["mean"] = total * scale
-        return scale
-    dqn_mod.allreduce_gradients = spy_allreduce
+        return None, scale   # already complete
+    dqn_mod.allreduce_gradients_async = spy_allreduce
     real_train_step = agent.train_step
 
-    def spy_train_step(tr, sync_loss=True, loss_out=None):
+    def spy_train_step(tr, sync_loss=True, loss_out=None, overlap=None):
         if rec["checked"] >= 3:
-            return real_train_step(tr, sync_loss=sync_loss, loss_out=loss_out)
+            return real_train_step(tr, sync_loss=sync_loss, loss_out=loss_out, overlap=overlap)
         m0 = agent.exp_avg.clone()
-        out = real_train_step(tr, sync_loss=sync_loss, loss_out=loss_out)
+        out = real_train_step(tr, sync_loss=sync_loss, loss_out=loss_out, overlap=overlap)
         expect = m0 + 0.1 * (rec["mean"] - m0)               # adam_kernel: m + (1 - b1)(g * scale - m)
         scale_ = m0.abs() + 0.1 * rec["mean"].abs() + 1e-30   # error relative to the terms (no cancellation)
         err = float(((agent.exp_avg - expect).abs() / scale_).max())
@@ -78,7 +80,7 @@ def main():
         return out
     agent.train_step = spy_train_step
     agent.learn(timesteps=B * world * 2 * n * 2)
-    dqn_mod.allreduce_gradients = real_allreduce
+    dqn_mod.allreduce_gradients_async = real_allreduce
     w = agent.network.flat.clone()
     allw = [torch.zeros_like(w) for _ in range(world)]
     dist.all_gather(allw, w)

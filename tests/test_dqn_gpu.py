@@ -317,6 +317,18 @@ def test_evaluate_agent_matches_oracle(metric):
         assert score == pytest.approx(np.mean(got_s), rel=1e-15) and sol == pytest.approx(np.mean(got_o), rel=1e-15)
     # the next call continues with the following graphs in order (ordered SetGraphGenerator)
     assert test_env._eval_next_graph == 0
+    # every test episode in one fill (4 episodes, 4 slots, lockstep): the sync-free path of evaluate_agent takes
+    # graphs 0..3 from the same spins as the first refill batch above, so it must reproduce those rollouts
+    agent.test_episodes = 4
+    score4, sol4 = agent.evaluate_agent()
+    got_s4, got_o4 = agent.last_evaluation
+    assert len(got_s4) == 4 and test_env._eval_next_graph == 4
+    for i, r in enumerate(res[:4]):
+        if r[5]:
+            continue
+        assert got_s4[i] == (r[col[0]] if col[0] is not None else 0.0), (i, got_s4[i], r)
+        assert got_o4[i] == (r[col[1]] if col[1] is not None else 0.0), (i, got_o4[i], r)
+    assert got_s4 == got_s[:4] and got_o4 == got_o[:4]
 
 
 def test_learn_evaluates_saves_and_pickles(tmp_path):
@@ -484,7 +496,6 @@ def test_learn_with_staggered_dones_resets_only_finished_episodes():
                 initial_learning_rate=1e-4, peak_learning_rate=1e-4, final_learning_rate=1e-4, update_frequency=32,
                 minibatch_size=64, final_exploration_rate=0.05, final_exploration_step=20000, seed=21,
                 evaluate=False, test_save_path=None, graph_pool_ids=pool)
-    assert not agent._lockstep
     hist = {"partial": 0}
     prev = {}
 
@@ -503,6 +514,7 @@ def test_learn_with_staggered_dones_resets_only_finished_episodes():
         prev["gids"], prev["steps"] = gids, steps
 
     first = agent.learn(timesteps=B * 60, on_vector_step=watch)
+    assert not agent._lockstep
     assert hist["partial"] > 0, "no staggered resets happened"
     assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()
     n1 = len(agent.losses())

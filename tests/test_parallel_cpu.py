@@ -23,13 +23,20 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from eco_hip.parallel import (allreduce_gradients, broadcast_parameters, max_over_ranks,
-                                      best_cut_over_ranks, rank_seed)
+        from eco_hip.parallel import (allreduce_gradients, allreduce_gradients_async, broadcast_parameters,
+                                      max_over_ranks, best_cut_over_ranks, rank_seed)
         # gradient all-reduce: sum, scale 1/world
         g = torch.full((58425,), float(rank + 1))
         scale = allreduce_gradients(g)
         assert scale == 1.0 / world
         assert torch.all(g == sum(range(1, world + 1)))
+        # the overlapped form (DQN.train_step): start, independent work, wait -> the same sum
+        g2 = torch.full((58425,), float(10 * (rank + 1)))
+        work, scale2 = allreduce_gradients_async(g2)
+        other = torch.arange(1000.0).sum()   # independent work while the collective runs
+        assert work is not None and scale2 == 1.0 / world and float(other) == 499500.0
+        work.wait()
+        assert torch.all(g2 == 10 * sum(range(1, world + 1)))
         # parameter broadcast from rank 0
         p = torch.randn(58425, generator=torch.Generator().manual_seed(rank_seed(7, rank)))
         broadcast_parameters(p)

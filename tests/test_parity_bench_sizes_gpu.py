@@ -194,17 +194,17 @@ def test_learn_er200_first_train_step_matches_oracle():
     rec = {}
     orig = agent.train_step
 
-    def spy(tr, sync_loss=True, loss_out=None):
+    def spy(tr, sync_loss=True, loss_out=None, overlap=None):
         if not rec:
             rec["tr"] = [t.clone() for t in tr]
             rec["w"] = _flat_to_dict(agent.network.flat.clone())
             rec["tw"] = _flat_to_dict(agent.target_network.flat.clone())
-            loss = orig(tr, sync_loss=True, loss_out=loss_out)
+            loss = orig(tr, sync_loss=True, loss_out=loss_out, overlap=overlap)
             rec["loss"] = loss
             rec["grad"] = _flat_to_dict(agent.grad.clone())
             rec["w1"] = _flat_to_dict(agent.network.flat.clone())
             return torch.tensor([loss], device="cuda")
-        return orig(tr, sync_loss=sync_loss, loss_out=loss_out)
+        return orig(tr, sync_loss=sync_loss, loss_out=loss_out, overlap=overlap)
 
     agent.train_step = spy
     agent.learn(timesteps=B * 4)
@@ -254,17 +254,17 @@ def test_learn_ba500_first_train_step_matches_oracle():
     rec = {}
     orig = agent.train_step
 
-    def spy(tr, sync_loss=True, loss_out=None):
+    def spy(tr, sync_loss=True, loss_out=None, overlap=None):
         if not rec:
             rec["tr"] = [t.clone() for t in tr]
             rec["w"] = _flat_to_dict(agent.network.flat.clone())
             rec["tw"] = _flat_to_dict(agent.target_network.flat.clone())
-            loss = orig(tr, sync_loss=True, loss_out=loss_out)
+            loss = orig(tr, sync_loss=True, loss_out=loss_out, overlap=overlap)
             rec["loss"] = loss
             rec["grad"] = _flat_to_dict(agent.grad.clone())
             rec["w1"] = _flat_to_dict(agent.network.flat.clone())
             return torch.tensor([loss], device="cuda")
-        return orig(tr, sync_loss=sync_loss, loss_out=loss_out)
+        return orig(tr, sync_loss=sync_loss, loss_out=loss_out, overlap=overlap)
 
     agent.train_step = spy
     agent.learn(timesteps=B * 3)
