@@ -67,13 +67,18 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
   const f32x2v v = {a, b};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));  // v_cvt_pk_f16_f32 (RNE)
 }
-// (a, b) already scaled into fp16 range -> hi and lo fp16 pairs with a = hi + lo to 2^-22
-__device__ __forceinline__ void split2_pk(float a, float b, uint32_t& hi, uint32_t& lo) {
-  hi = pk_f16(a, b);
-  const f32x2v back = __builtin_convertvector(__builtin_bit_cast(f16x2v, hi), f32x2v);
-  const f32x2v v = {a, b};
-  const f32x2v r = v - back;  // exact (Sterbenz / subnormal remainder)
-  lo = pk_f16(r[0], r[1]);
+// (a, b) scaled by the power of two sf into fp16 range -> hi and lo fp16 pairs with a sf = hi + lo to 2^-22.
+// lo = fp16(a sf - hi) in ONE v_fma_mix{lo,hi}_f16 per value (f32 a and sf, f16 hi, single rounding: a sf - hi
+// is exact, so the result is bitwise that of converting hi back, subtracting and converting: 4 VALU per pair
+// instead of 6, the per-layer split being the largest VALU item of the dense kernels)
+__device__ __forceinline__ void split2_pk(float a, float b, float sf, uint32_t& hi, uint32_t& lo) {
+  hi = pk_f16(a * sf, b * sf);
+  uint32_t l;  // mixlo writes bits 15:0 (16:31 kept, then written by mixhi)
+  // the trailing s_nop: the hazard recognizer does not see inside inline asm, and an MFMA reading a VGPR written
+  // by VALU needs 2 wait states (without it the fragments fed to the MFMAs were stale in some schedules)
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(sf), "v"(hi));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1" : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
+  lo = l;
 }
 // 2^k as a float (k clamped to the normal range)
 __device__ __forceinline__ float exp2i(int k) {
@@ -113,10 +118,10 @@ __device__ __forceinline__ float absmax4(const float4& v, float m) {
 // 8 activations (float4 c = 2kc2, 2kc2+1 of a 64-input half) scaled by sf, as hi / lo fp16 B fragments
 __device__ __forceinline__ void split_fh(const float4& a, const float4& b, float sf, f16x8& hi, f16x8& lo) {
   uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
-  split2_pk(a.x * sf, a.y * sf, h0, l0);
-  split2_pk(a.z * sf, a.w * sf, h1, l1);
-  split2_pk(b.x * sf, b.y * sf, h2, l2);
-  split2_pk(b.z * sf, b.w * sf, h3, l3);
+  split2_pk(a.x, a.y, sf, h0, l0);
+  split2_pk(a.z, a.w, sf, h1, l1);
+  split2_pk(b.x, b.y, sf, h2, l2);
+  split2_pk(b.z, b.w, sf, h3, l3);
   const u32x4v h = {h0, h1, h2, h3}, l = {l0, l1, l2, l3};
   hi = __builtin_bit_cast(f16x8, h);
   lo = __builtin_bit_cast(f16x8, l);
@@ -205,11 +210,11 @@ __device__ __forceinline__ int tile_exp(const float4 (&v)[4]) {
   const float mx = wave_max_nonneg(m);
   return mx > 0.f ? scale_exp(mx) : D2_K_EMPTY;
 }
-// features 16ft + 4k .. +3 of node j, already scaled, as two fp16 planes
-__device__ __forceinline__ void plane2_store4(uint16_t* P0, uint16_t* P1, int ft, int j, int k, float4 v) {
+// features 16ft + 4k .. +3 of node j, scaled by sf, as two fp16 planes
+__device__ __forceinline__ void plane2_store4(uint16_t* P0, uint16_t* P1, int ft, int j, int k, float4 v, float sf) {
   uint32_t h0, l0, h1, l1;
-  split2_pk(v.x, v.y, h0, l0);
-  split2_pk(v.z, v.w, h1, l1);
+  split2_pk(v.x, v.y, sf, h0, l0);
+  split2_pk(v.z, v.w, sf, h1, l1);
   const int o = plane_off(ft, j, k);
   *reinterpret_cast<uint2*>(P0 + o) = make_uint2(h0, h1);
   *reinterpret_cast<uint2*>(P1 + o) = make_uint2(l0, l1);
@@ -221,7 +226,7 @@ __device__ __forceinline__ void tile_planes(uint16_t* P0, uint16_t* P1, int* TE,
   const float sf = exp2i(k == D2_K_EMPTY ? 0 : k);
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    plane2_store4(P0, P1, c, r, s4, make_float4(v[c].x * sf, v[c].y * sf, v[c].z * sf, v[c].w * sf));
+    plane2_store4(P0, P1, c, r, s4, v[c], sf);
   if (lane == 0) TE[tile] = k;
 }
 

@@ -61,8 +61,8 @@ __device__ __forceinline__ void dl_planes_half(uint16_t* P0, uint16_t* P1, int j
   for (int ftl = 0; ftl < 2; ++ftl) {
     const float4 v = ftl ? v1 : v0;
     uint32_t h0, l0, h1, l1;
-    split2_pk(v.x * sf, v.y * sf, h0, l0);
-    split2_pk(v.z * sf, v.w * sf, h1, l1);
+    split2_pk(v.x, v.y, sf, h0, l0);
+    split2_pk(v.z, v.w, sf, h1, l1);
     const int o = dl_plane_off(ftl, j, s4);
     *reinterpret_cast<uint2*>(P0 + o) = make_uint2(h0, h1);
     *reinterpret_cast<uint2*>(P1 + o) = make_uint2(l0, l1);
