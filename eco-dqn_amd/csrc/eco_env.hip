@@ -154,6 +154,43 @@ __device__ __forceinline__ void write_obs(const EnvArgs& a, int e, int lane, con
   }
 }
 
+// write_obs for DEFAULT_OBSERVABLES (spinsystem.py:486-535 with the ECO training observables, the hot path) and no
+// float64 rows: the fp32 feature rows directly.  Per vertex only three values vary -- the spin (basis-mapped), the
+// immediate quality change g / mlr and the time since flip -- and the other four are wave-uniform, converted
+// once.  g / mlr is the correctly rounded f32 quotient of the two integers (exact in f32: |g|, |mlr| < 2^18),
+// which equals the reference's float64 quotient rounded to f32: the exact quotient of integers below 2^18 is
+// never within 2^-53 of an f32 rounding midpoint without being one (its distance from any K / 2^j is at least
+// 2^-42 relative), so rounding through float64 cannot change the f32 result.  -0.0 is kept (the product is a
+// float product: s = -1, h = 0 gives -0.0, as the reference's float64 product does).  tests/test_env_gpu.py
+// checks these rows bitwise against the general path.
+__device__ __forceinline__ bool obs_default_layout(const eco_env_config& c) {
+  return c.n_obs == 7 && c.obs_ids[0] == ECO_OBS_SPIN_STATE && c.obs_ids[1] == ECO_OBS_IMMEDIATE_QUALITY_CHANGE &&
+         c.obs_ids[2] == ECO_OBS_TIME_SINCE_FLIP && c.obs_ids[3] == ECO_OBS_DISTANCE_FROM_BEST_SOLUTION &&
+         c.obs_ids[4] == ECO_OBS_DISTANCE_FROM_BEST_STATE && c.obs_ids[5] == ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS &&
+         c.obs_ids[6] == ECO_OBS_TERMINATION_IMMANENCY;
+}
+template <int VPT>
+__device__ __forceinline__ void write_obs_default(const EnvArgs& a, int e, int lane, const int (&s)[VPT],
+                                                  const int (&h)[VPT], const int (&tsf)[VPT], const ObsCtx& c) {
+  const int N = a.cfg.n_spins;
+  const double* tab = tab_ptr(a);
+  const float mlrf = (float)c.mlr;
+  const float u3 = (float)c.dist_best, u4 = (float)c.hamming, u5 = (float)c.nqi, u6 = (float)c.term;
+  const bool binary = c.basis == ECO_BASIS_BINARY;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int v = lane + 64 * k;
+    if (v >= N) continue;
+    const float sf = (float)s[k];
+    const float x0 = binary ? (float)((1 - s[k]) / 2) : sf;  // (1 - s) / 2 is exact: 0 or 1
+    const float x1 = __fdiv_rn(sf * (float)h[k], mlrf);
+    const float x2 = (float)tab[tsf[k]];
+    float4* dst = (float4*)(a.obs_x + ((size_t)e * N + v) * 8);
+    dst[0] = make_float4(x0, x1, x2, u3);
+    dst[1] = make_float4(u4, u5, u6, 0.f);
+  }
+}
+
 // SpinSystemBase.reset (spinsystem.py:183-259) + _reset_state (:283-330)
 template <int VPT>
 __global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
@@ -253,14 +290,31 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvArgs a) {
   write_obs<VPT>(a, e, lane, s, h, tsf, c);
 }
 
+// Optional per-phase stamps of env_step_kernel (timing build only: make timing; tools/r04/env_timing.py):
+// [episode][8] wall_clock64 values, first ECO_ENV_TS_EPS episodes.
+#ifdef ECO_PHASE_TIMING
+constexpr int ECO_ENV_TS_EPS = 16384;
+__device__ unsigned long long eco_env_ts[ECO_ENV_TS_EPS * 8];
+#define ECO_ENV_TS(k)                                                                                      \
+  do {                                                                                                    \
+    if (lane == 0 && e < ECO_ENV_TS_EPS) eco_env_ts[e * 8 + (k)] = wall_clock64();                        \
+  } while (0)
+#else
+#define ECO_ENV_TS(k) \
+  do {                \
+  } while (0)
+#endif
+
 // SpinSystemBase.step (spinsystem.py:355-559), ExtraAction.NONE, memory_length None.
-template <int VPT>
-__global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
+// FASTOBS: DEFAULT_OBSERVABLES, fp32 rows only (write_obs_default).
+template <int VPT, bool FASTOBS>
+__device__ __forceinline__ void env_step_body(const EnvArgs& a) {
   extern __shared__ int32_t d_lds[];  // [4 waves][N] row deltas
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int e = uniform_i(blockIdx.x * 4 + wv);
   if (e >= a.B) return;
+  ECO_ENV_TS(0);
   const int N = a.cfg.n_spins;
   const int T = a.cfg.max_steps;
   const EnvLayout& L = a.L;
@@ -292,13 +346,18 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   }
   int sa_old, ha;
   read_vertex<VPT>(s, h, act, sa_old, ha);
+  ECO_ENV_TS(1);
   const double qn = sc->qn, mlr = sc->mlr;
   const double delta = (double)sa_old * (double)ha;  // f64 product: keeps -0.0 like the reference
   const double delta_n = delta / qn;     // get_normalized_score_mask(state)[action] (:394)
   const double score = sc->score + delta;           // :399
   const double nscore = sc->nscore + delta_n;       // :400 (accumulated)
   // incremental local field: h_j -= 2 w_aj s_a(old) over the CSR row of `act`
-  row_update<VPT>(d_lds + wv * N, ed, q0, q1, N, lane, h, [&](int w) { return -2 * w * sa_old; });
+  const bool track = a.cfg.has_basin_reward || a.cfg.has_stag_punishment;
+  HistProbe hp;
+  row_update<VPT>(d_lds + wv * N, ed, q0, q1, N, lane, h, [&](int w) { return -2 * w * sa_old; },
+                  [&] { if (track) history_probe(a, e, sc->hash, act, hp); });
+  ECO_ENV_TS(2);
   // flip + time-since-flip counters (:397, :492-497)
   int cnt = 0;
   uint64_t words[VPT];
@@ -315,8 +374,8 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) c += __popcll(__ballot(s[k] < 0)); return c; }();
   // HistoryBuffer.update (utils.py:444-464): is the flipped set (== spin configuration) new?
-  const bool isnew = (a.cfg.has_basin_reward || a.cfg.has_stag_punishment) ? history_update<VPT>(a, e, lane, sc, act, words)
-                                                                            : true;
+  const bool isnew = track ? history_update_from<VPT>(a, e, lane, sc, hp, words) : true;
+  ECO_ENV_TS(3);
   // reward (:418-457)
   double best_score = sc->best_score, best_nscore = sc->best_nscore;
   double rew = 0.0;
@@ -365,6 +424,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
     a.rewards[e] = rew;
     a.dones[e] = done ? 1 : 0;
   }
+  ECO_ENV_TS(4);
   ObsCtx c;
   c.mlr = mlr;
   const double dsc = score - best_score;
@@ -375,7 +435,20 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
   c.term = x > 0.0 ? x : 0.0;                                         // :509-511
   c.ep_time = tab_ptr(a)[t];                                          // :506
   c.basis = a.cfg.spin_basis;
-  write_obs<VPT>(a, e, lane, s, h, tsf, c);
+  if (FASTOBS) write_obs_default<VPT>(a, e, lane, s, h, tsf, c);
+  else write_obs<VPT>(a, e, lane, s, h, tsf, c);
+  ECO_ENV_TS(5);
+}
+template <int VPT, bool FASTOBS>
+__global__ __launch_bounds__(256) void env_step_kernel(EnvArgs a) {
+  env_step_body<VPT, FASTOBS>(a);
+}
+// The training / bench configuration up to N = 256 at 8 waves per SIMD (<= 64 VGPRs, no spills): all 8192
+// ER-200 episodes of a step are resident at once (one wave each) instead of 6144 plus a second round of 2048
+// (tools/r04/env_timing.py); above 4 vertices per lane that budget spills, so larger N runs env_step_kernel
+template <int VPT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void env_step_fast_kernel(EnvArgs a) {
+  env_step_body<VPT, true>(a);
 }
 
 // Greedy solver action (src/agents/solver.py:100-131): the vertex with the largest immediate
@@ -591,6 +664,13 @@ extern "C" int eco_env_reset(const eco_env_config* cfg, const eco_graph_set* gs,
   return check_launch("env_reset");
 }
 
+#ifdef ECO_PHASE_TIMING
+extern "C" int eco_debug_env_ts(unsigned long long* host, int32_t n) {
+  if (n > ECO_ENV_TS_EPS * 8) n = ECO_ENV_TS_EPS * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(eco_env_ts), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int eco_check_errors(eco_stream_t stream) {
   int32_t* w = err_word();
   if (!w) return fail(ECO_ERR_HIP, "cannot allocate error word");
@@ -609,7 +689,19 @@ extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, 
   hipStream_t st = (hipStream_t)stream;
   const int blocks = (batch + 3) / 4;
   if (generic_target(cfg)) return env_step_problem_launch(a, blocks, env_step_lds(cfg->n_spins), st);
-  ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V><<<blocks, 256, (size_t)16 * cfg->n_spins, st>>>(a)));
+  // the DEFAULT_OBSERVABLES fp32-only path (the training / bench configuration) or the general one
+  const bool fast = !obs_f64 && obs_x && cfg->n_obs == 7 && cfg->obs_ids[0] == ECO_OBS_SPIN_STATE &&
+                    cfg->obs_ids[1] == ECO_OBS_IMMEDIATE_QUALITY_CHANGE && cfg->obs_ids[2] == ECO_OBS_TIME_SINCE_FLIP &&
+                    cfg->obs_ids[3] == ECO_OBS_DISTANCE_FROM_BEST_SOLUTION &&
+                    cfg->obs_ids[4] == ECO_OBS_DISTANCE_FROM_BEST_STATE &&
+                    cfg->obs_ids[5] == ECO_OBS_NUMBER_OF_QUALITY_IMPROVEMENTS &&
+                    cfg->obs_ids[6] == ECO_OBS_TERMINATION_IMMANENCY;
+  const size_t lds = (size_t)16 * cfg->n_spins;
+  if (fast && cfg->n_spins <= 64) env_step_fast_kernel<1><<<blocks, 256, lds, st>>>(a);
+  else if (fast && cfg->n_spins <= 128) env_step_fast_kernel<2><<<blocks, 256, lds, st>>>(a);
+  else if (fast && cfg->n_spins <= 256) env_step_fast_kernel<4><<<blocks, 256, lds, st>>>(a);
+  else if (fast) ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V, true><<<blocks, 256, lds, st>>>(a)));
+  else ECO_DISPATCH_VPT(cfg->n_spins, (env_step_kernel<V, false><<<blocks, 256, lds, st>>>(a)));
   return check_launch("env_step");
 }
 

@@ -82,18 +82,29 @@ __device__ __forceinline__ void read_vertex(const int (&s)[VPT], const int (&f)[
 // f_j += coef(J_ja) for every neighbour j of `act`: the lanes load the CSR row in parallel and scatter the
 // deltas through the wave's LDS slice dl[N] (a row has distinct columns, so the stores never collide) --
 // one round of loads instead of deg(a) dependent ones.
-template <int VPT, class Coef>
+struct NoIssue {
+  __device__ void operator()() const {}
+};
+// after_loads: issued right after the row's edge loads (the step's next loads, e.g. the visited-set probe)
+template <int VPT, class Coef, class After = NoIssue>
 __device__ __forceinline__ void row_update(int32_t* dl, const uint32_t* ed, int q0, int q1, int N, int lane,
-                                           int (&f)[VPT], Coef coef) {
+                                           int (&f)[VPT], Coef coef, After after_loads = After()) {
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int v = lane + 64 * k;
     if (v < N) dl[v] = 0;
   }
   wave_lds_sync();
-  for (int q = q0 + lane; q < q1; q += 64) {
-    const uint32_t x = ed[q];
-    dl[edge_col(x)] = coef(edge_w(x));
+  if (q1 - q0 <= 64) {  // one load per lane (every ER-200 / BA-500 row): the caller's next loads go out behind it
+    const uint32_t x = q0 + lane < q1 ? ed[q0 + lane] : 0u;
+    after_loads();
+    if (q0 + lane < q1) dl[edge_col(x)] = coef(edge_w(x));
+  } else {
+    after_loads();
+    for (int q = q0 + lane; q < q1; q += 64) {
+      const uint32_t x = ed[q];
+      dl[edge_col(x)] = coef(edge_w(x));
+    }
   }
   wave_lds_sync();
 #pragma unroll
@@ -140,6 +151,64 @@ __device__ __forceinline__ bool history_update(const EnvArgs& a, int e, int lane
       for (int k = 0; k < VPT; ++k)
         if (k < W) vst[(size_t)n * W + k] = words[k];  // VPT = next power of two >= W
       vh[slot] = hash;
+      vidx[slot] = (uint32_t)(n + 1);
+      sc->visit_count = n + 1;
+    }
+  }
+  return isnew;
+}
+
+// The same update with the first probe slot loaded ahead by the caller (history_probe, issued right after the
+// step's CSR-row loads so its latency runs under the field update and the ballots; vmcnt is in order, so issuing
+// it before loads the step needs sooner would delay those instead).
+struct HistProbe {
+  uint64_t hash;
+  int slot;
+  uint32_t id;
+  uint64_t hs;
+};
+__device__ __forceinline__ void history_probe(const EnvArgs& a, int e, uint64_t prev_hash, int act, HistProbe& p) {
+  const EnvLayout& L = a.L;
+  const int cap = L.cap;
+  p.hash = prev_hash ^ zobrist(act);
+  p.slot = (int)(p.hash & (uint64_t)(cap - 1));
+  p.id = ((const uint32_t*)(a.state + L.off_vidx) + (size_t)e * cap)[p.slot];
+  p.hs = ((const uint64_t*)(a.state + L.off_vhash) + (size_t)e * cap)[p.slot];
+}
+template <int VPT>
+__device__ __forceinline__ bool history_update_from(const EnvArgs& a, int e, int lane, EpScal* sc, const HistProbe& p,
+                                                    const uint64_t (&words)[VPT]) {
+  const EnvLayout& L = a.L;
+  const int T = a.cfg.max_steps;
+  const int cap = L.cap;
+  const int W = L.words;
+  uint32_t* vidx = (uint32_t*)(a.state + L.off_vidx) + (size_t)e * cap;
+  uint64_t* vh = (uint64_t*)(a.state + L.off_vhash) + (size_t)e * cap;
+  uint64_t* vst = (uint64_t*)(a.state + L.off_vstates) + (size_t)e * (T + 1) * W;
+  bool isnew = true;
+  int slot = p.slot;
+  uint32_t id = p.id;
+  uint64_t hs = p.hs;
+  for (;;) {
+    if (id == 0u) break;
+    if (hs == p.hash) {
+      bool same = true;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) same = same && (k >= W || vst[(size_t)(id - 1) * W + k] == words[k]);
+      if (same) { isnew = false; break; }
+    }
+    slot = (slot + 1) & (cap - 1);
+    id = vidx[slot];
+    hs = vh[slot];
+  }
+  if (lane == 0) {
+    sc->hash = p.hash;
+    if (isnew) {
+      const int n = sc->visit_count;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k)
+        if (k < W) vst[(size_t)n * W + k] = words[k];
+      vh[slot] = p.hash;
       vidx[slot] = (uint32_t)(n + 1);
       sc->visit_count = n + 1;
     }
