@@ -186,51 +186,52 @@ class RandomBarabasiAlbertGraphGenerator(GraphGenerator):
         return _symmetric(n, iu, ju, _edge_weights(self.edge_type, iu.size))
 
 
-class SingleGraphGenerator(GraphGenerator):
-    """src/envs/utils.py:319-345"""
-
-    def __init__(self, matrix, bias=None):
-        n_spins = matrix.shape[0]
-        if np.isin(matrix, [0, 1]).all():
-            edge_type = EdgeType.UNIFORM
-        elif np.isin(matrix, [0, -1, 1]).all():
-            edge_type = EdgeType.DISCRETE
-        else:
-            edge_type = EdgeType.RANDOM
-        super().__init__(n_spins, edge_type, bias is not None)
-        self.matrix = matrix
-        self.bias = bias
-
-    def get(self, with_padding=False):
-        if self.biased:
-            return self.matrix, self.bias
-        return self.matrix
+def _edge_type_of(matrices):
+    """EdgeType of a collection of adjacency matrices, from the set of weights they use: {0, 1} -> UNIFORM,
+    {0, +-1} -> DISCRETE, anything else -> RANDOM (the classification the reference's known-graph generators
+    make, src/envs/utils.py:323-330, :351-358)."""
+    weights = set()
+    for m in matrices:
+        weights.update(np.unique(np.asarray(m)).tolist())
+    if weights <= {0, 1}:
+        return EdgeType.UNIFORM
+    if weights <= {0, -1, 1}:
+        return EdgeType.DISCRETE
+    return EdgeType.RANDOM
 
 
 class SetGraphGenerator(GraphGenerator):
-    """src/envs/utils.py:347-382 (ordered cycles through the set; unordered samples with python `random`)."""
+    """Known graphs of one size (src/envs/utils.py:347-382): `ordered` hands them out in turn, cycling; otherwise
+    each get() draws one uniformly with python's `random` module (the stream set_global_seed seeds, consumed as
+    the reference's random.sample(graphs, k=1) consumes it).  With biases, get() returns (matrix, bias) pairs."""
 
     def __init__(self, matrices, biases=None, ordered=False):
-        if len(set([m.shape[0] - 1 for m in matrices])) == 1:
-            n_spins = matrices[0].shape[0]
-        else:
+        matrices = list(matrices)
+        if len({np.asarray(m).shape[0] for m in matrices}) != 1:
             raise NotImplementedError("All graphs in SetGraphGenerator must have the same dimension.")
-        if all([np.isin(m, [0, 1]).all() for m in matrices]):
-            edge_type = EdgeType.UNIFORM
-        elif all([np.isin(m, [0, -1, 1]).all() for m in matrices]):
-            edge_type = EdgeType.DISCRETE
+        super().__init__(np.asarray(matrices[0]).shape[0], _edge_type_of(matrices), biases is not None)
+        if self.biased:
+            biases = list(biases)
+            assert len(biases) == len(matrices), "Must pass through the same number of matrices and biases."
+            assert all(len(b) == self.n_spins + 1 for b in biases), \
+                "All biases and must have the same dimension as the matrices."
+            self.graphs = list(zip(matrices, biases))
         else:
-            edge_type = EdgeType.RANDOM
-        super().__init__(n_spins, edge_type, biases is not None)
-        self.graphs = matrices
+            self.graphs = matrices
         self.ordered = ordered
-        if self.ordered:
-            self.i = 0
+        self.i = 0
 
     def get(self, with_padding=False):
-        if self.ordered:
-            m = self.graphs[self.i]
-            self.i = (self.i + 1) % len(self.graphs)
-        else:
-            m = random.sample(self.graphs, k=1)[0]
-        return m
+        if not self.ordered:
+            return self.graphs[random.sample(range(len(self.graphs)), 1)[0]]
+        item = self.graphs[self.i]
+        self.i = (self.i + 1) % len(self.graphs)
+        return item
+
+
+class SingleGraphGenerator(SetGraphGenerator):
+    """One known graph (src/envs/utils.py:319-345): every get() returns it (with its bias, when given)."""
+
+    def __init__(self, matrix, bias=None):
+        super().__init__([matrix], None if bias is None else [bias], ordered=True)
+        self.matrix, self.bias = matrix, bias
