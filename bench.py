@@ -340,12 +340,32 @@ def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000):
     agent.evaluate_agent()
     torch.cuda.synchronize()
     eval_ms = (time.perf_counter() - t0) * 1e3
+    # learn()'s default: the evaluation overlapped with training (DQN._evaluate_overlapped, side stream on a
+    # snapshot of the weights).  Its cost = the wall time it adds to the vector steps it runs beside.
+    k = 8
+    agent._eval_one_fill_finish(agent._evaluate_overlapped(0))  # allocations
+    ts = []
+    for ov in (False, True, False, True):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p = agent._evaluate_overlapped(0) if ov else None
+        for _ in range(k):
+            agent.iteration()
+        if p is not None:
+            agent._eval_one_fill_finish(p)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ov_ms = max(0.0, (ts[1] + ts[3] - ts[0] - ts[2]) / 2)
     agent.test_envs, agent.test_episodes, agent.test_metric = saved
-    per_vec = reset_ms / T + eval_ms * (B * world / test_frequency)
+    per_vec_sync = reset_ms / T + eval_ms * (B * world / test_frequency)
+    per_vec = reset_ms / T + ov_ms * (B * world / test_frequency)
     return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T,
-            "evaluate_agent_ms": eval_ms, "evaluate_every_env_steps": test_frequency,
+            "evaluate_agent_ms": eval_ms, "evaluate_overlapped_ms": ov_ms,
+            "evaluate_overlapped_note": f"wall time one overlapped evaluation adds to {k} vector steps of training "
+                                        "(learn()'s default; evaluate_agent_ms is the synchronous call)",
+            "evaluate_every_env_steps": test_frequency,
             "evaluate_setting": f"{test_graphs} ER-{n} test graphs, BEST metric, {T} greedy steps each",
-            "amortised_ms_per_vector_step": per_vec,
+            "amortised_ms_per_vector_step": per_vec, "amortised_ms_per_vector_step_sync_eval": per_vec_sync,
             "note": "not in the timed region: amortised, these would add this many ms to ms_per_step"}
 
 

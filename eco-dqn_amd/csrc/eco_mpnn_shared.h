@@ -5,15 +5,17 @@
 // gather of each episode's 256-B fp32 row re-reads nnz x B x 256 B per layer (10.5 GB at G22 x 1024), and
 // served from L2 at its gather ceiling (~15 TB/s measured, MI355X_MICROARCH.md 'Indexed rows': 16.8-18.8)
 // that was 0.84 ms per layer.  Here an aggregation launch stages ONE feature chunk of ONE episode -- the
-// [N][16] fp32 block, 128 KB at N = 2000 -- in LDS with one contiguous read, and every node's neighbour sum
-// is taken from LDS (ds_read_b128 per edge), nodes in 16-node tiles of similar degree walking their CSR rows
-// in lockstep: HBM/L2 traffic per layer is one read and one write of H (2 x 0.5 GB) plus the CSR words.
+// [N][8] fp32 block, 64 KB at N = 2000 -- in LDS with one contiguous read, and every node's neighbour sum
+// is taken from LDS (ds_read_b128 per edge and lane pair), nodes in 16-node tiles of similar degree walking
+// their CSR rows in lockstep.  The graph's CSR words (16-bit, interleaved per tile) are LDS-resident too, loaded
+// once per persistent workgroup (85 KB on G22-like graphs; graphs whose table does not fit next to the block
+// read it from L2): HBM/L2 traffic per layer is one read and one write of H (2 x 0.5 GB).
 // The Linears then run as a streaming pass over rows (no gathers): 16-row MFMA tiles of 4 consecutive
 // nodes x 4 episodes, weights LDS-DMA-staged once per persistent workgroup.
 //
-// Layout: every per-node buffer is [slice s][feature chunk c][episode e of the slice][node][16 floats]:
-// an aggregation item (s, c, e) is one contiguous N x 64 B block, and a Linear tile's rows of one chunk are
-// SH_EPS runs of 4 consecutive nodes x 64 B = 256 B.
+// Layout: every per-node buffer is [slice s][feature chunk c of 8][episode e of the slice][node][8 floats]:
+// an aggregation item (s, c, e) is one contiguous N x 32 B block, and a Linear tile's rows of one chunk are
+// SH_EPS runs of 4 consecutive nodes x 32 B = 128 B.
 //
 // Phases (one launch each; U = relu(Wx.x + w_a), V = relu(Wx.x - w_a) and h0 = relu(W0.x) are never stored:
 // the aggregation launches build their blocks from the 32-B observation rows, the first update layer its
@@ -24,15 +26,19 @@
 //            per-episode column sums of h3 (fixed-order partials per tile)
 //   readout: mean -> p = Wp.mean -> q = relu(p).Wr[:64] + q_local + b, fused epsilon-greedy act
 //            (mpnn.py:143-159, dqn.py:453-465, :490-512)
-// Linears: the six-product bf16x3 MFMAs of the dense kernels (f32-accurate).  Integer weights must be
+// Linears: the three-product fp16x2 MFMAs of eco_mpnn_dense2.h (f32-accurate; per-node scale over the Linear's
+// inputs, pre-split weights PK_FH).  Integer weights must be
 // +-1 (the edge phase sums U over +1 edges and V over -1 edges); other graphs take mpnn_forward_large_kernel.
 #pragma once
-#include "eco_mpnn_dense.h"
+#include "eco_mpnn_dense2.h"
 
 namespace eco {
 
 #ifndef SH_NW_X
 #define SH_NW_X 16
+#endif
+#ifndef ECO_AB_SHARED_BF3
+#define ECO_AB_SHARED_BF3 0            // A/B builds only (tools/): the round-3 six-product bf16x3 Linears
 #endif
 constexpr int SH_EPS = 4;              // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per Linear tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
@@ -47,18 +53,11 @@ constexpr int SH_PART = SH_EPS * 64;   // floats of one tile's column-sum partia
 #define AG_NW_X 16
 #endif
 constexpr int AG_NW = AG_NW_X;         // waves per aggregation workgroup (8: 256 VGPRs for the block prefetch)
-#ifndef AG_UNROLL_X
-#define AG_UNROLL_X 4
-#endif
 #ifndef AG_TPW_X
 #define AG_TPW_X 2
 #endif
-constexpr int AG_TPW = AG_TPW_X;       // aggregation tiles per wave in flight together
-#ifndef AG_DEPTH2
-#define AG_DEPTH2 0                    // 1: edge words loaded two groups ahead instead of one
-#endif
-constexpr int AG_UNROLL = AG_UNROLL_X; // edge words in flight per lane
-static_assert(AG_UNROLL % 4 == 0, "edge words are loaded in 16-B groups");
+constexpr int AG_TPW = AG_TPW_X;       // aggregation tile pairs per wave in flight together
+constexpr int AG_UNROLL = 4;           // a tile's rows are padded to multiples of 4 edges (one 8-B word group)
 
 struct SharedBufs {
   float* HA;      // [S][4][SH_EPS][N][16]: h2 (h0, U and V are never stored: the aggregation launches and the
@@ -72,6 +71,8 @@ struct SharedBufs {
   int32_t* tml;   // [nt16] the tile's longest CSR row, rounded up to AG_UNROLL
   uint32_t* et;   // [nt16][MD / 4][16][4] the tile's CSR rows interleaved, four consecutive edges of a slot in one
                   // 16-B word group (edge i of slot k at ((i >> 2) * 16 + k) * 4 + (i & 3); padding: 0)
+  uint16_t* et16; // the same words packed (tile t from toff[t], tml[t] x 16 words each) as sh_w16
+  int32_t* toff;  // [nt16 + 1] first 16-bit word of each tile in et16; toff[nt16] = the table's words
   const uint64_t* key;  // workspace header: [0] key of the cached perm / tile tables, [1] 1 = rebuild this call
   int Epad, S, ntiles, nt16, MD;
 };
@@ -91,7 +92,8 @@ inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
   const size_t nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   const size_t nt16 = ((size_t)N + 15) / 16, MD = ((size_t)N + 3) / 4 * 4 + AG_UNROLL;
-  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + 4 + nt16 * MD * 16) *
+  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + 4 + nt16 * MD * 16 +
+          nt16 * MD * 8 + nt16 + 1 + 4) *
          sizeof(float);
 }
 
@@ -113,15 +115,18 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.tn = sb.perm + N;
   sb.tml = sb.tn + (size_t)sb.nt16 * 16;
   sb.et = reinterpret_cast<uint32_t*>(((uintptr_t)(sb.tml + sb.nt16) + 15) & ~(uintptr_t)15);  // 16-B groups
+  sb.et16 = reinterpret_cast<uint16_t*>(sb.et + (size_t)sb.nt16 * sb.MD * 16);
+  sb.toff = reinterpret_cast<int32_t*>(sb.et16 + (size_t)sb.nt16 * sb.MD * 16);
   return sb;
 }
 
-// float offset of row (slice s, episode eps of the slice, node n), chunk 0, features 4 q ..; chunk c adds
-// c * sh_cs(N)
+constexpr int SH_FC = 8;  // features per chunk (8 chunks)
+// float offset of features 4 q .. 4 q + 3 of row (slice s, episode eps of the slice, node n): chunk q / 2 of the
+// 8-feature chunks; features 16 c + 4 q .. (the lane's float4 c of the node-operand layout) add c * sh_cs(N)
 __device__ __forceinline__ size_t sh_row(int N, int s, int eps, int n, int q) {
-  return (((size_t)s * 4 * SH_EPS + eps) * N + n) * 16 + 4 * q;
+  return (((size_t)s * 8 * SH_EPS + eps) * N + n) * SH_FC + (size_t)(q >> 1) * SH_EPS * N * SH_FC + 4 * (q & 1);
 }
-__device__ __forceinline__ size_t sh_cs(int N) { return (size_t)SH_EPS * N * 16; }
+__device__ __forceinline__ size_t sh_cs(int N) { return (size_t)2 * SH_EPS * N * SH_FC; }
 
 // streaming (non-temporal) row access: the layer's own e rows and its output rows are touched once, and
 // should not push the gathered slice of H out of the L2
@@ -154,6 +159,27 @@ __device__ __forceinline__ void mm_bf3_seq(f32x4 (&acc)[4], const float4 (&x)[4]
       acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, x1, acc[nt], 0, 0, 0);
       acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x2, acc[nt], 0, 0, 0);
       acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, x1, acc[nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// mm_fh of eco_mpnn_dense2.h (fp16x2 operands: the 64-input half of x scaled by the node's 2^kx, hi / lo pieces, three
+// products) with one output tile's fragments in flight at a time, for the same reason as mm_bf3_seq
+__device__ __forceinline__ void mm_fh_seq(f32x4 (&acc)[4], const float4 (&x)[4], float sf, const uint16_t* WH,
+                                          int lane) {
+  const uint16_t* wl = WH + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 xh, xl;
+    split_fh(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f16x8 w1 = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      const f16x8 w2 = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -238,33 +264,33 @@ __device__ __forceinline__ f32x4 lin8_chunk(const float* W, int c, float xk0, fl
 
 // aggregation tile tables: tile t, slot k -> node perm[16 t + k]; the tile's CSR rows interleaved (padding words
 // 0: column 0, weight 0) in a BANK-AWARE order, and the tile's longest row (slot 0: ranked first).
-// In shared_agg_kernel lane 4k + q reads 16 B of row col of slot k's current edge: a ds_read_b128 serves the lane
-// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63} (MI355X_MICROARCH.md
-// LDS) = slots {0,3,5,6}, {1,2,4,7}, {8,11,13,14}, {9,10,12,15}, each group four 64-B rows, whose bank quarter is
-// col mod 4.  In CSR order two of the four rows share a quarter at most steps (2.1 LDS cycles per group and
-// step on G22-like ER(2000, 0.01), 48 % of the kernel's LDS cycles measured as bank conflicts).  So one thread
-// per (tile, group) orders its four rows greedily: at every step each slot (fewest residue classes left first)
-// takes its next edge of a quarter no other slot of the group uses at that step -- the class with most edges
-// left -- or, with none free, of the least-used quarter (1.28 cycles per group-step on that graph; no step is
-// added: a row keeps its length).  The neighbour sums change summation order only.
+// In shared_agg_kernel lane 2k + q reads 16 B of the 32-B row col of slot k's current edge (a wave: slots 0..15
+// of one tile, then of the pair's second tile): a ds_read_b128 serves the lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31}, ... (MI355X_MICROARCH.md LDS) = slots {0,1,6,7,10,11,12,13} and {2,3,4,5,8,9,14,15} of each
+// tile, each group eight 32-B rows, whose bank eighth is col mod 8.  Random columns put ~2.4 LDS cycles on a group
+// and step; so one thread per (tile, group) orders its eight rows greedily: at every step each slot (fewest residue
+// classes left first) takes its next edge of an eighth no other slot of the group uses at that step -- the class
+// with most edges left -- or, with none free, of the least-used eighth (most edges left on ties); no step is added:
+// a row keeps its length.  The neighbour sums change summation order only.
 __device__ __forceinline__ int sh_group_slot(int g, int j) {
-  constexpr uint32_t tab[4] = {0x6530u, 0x7421u, 0xEDB8u, 0xFCA9u};  // slot of position j: nibble j
+  constexpr uint32_t tab[2] = {0xDCBA7610u, 0xFE985432u};  // slot of position j: nibble j
   return (tab[g] >> (4 * j)) & 0xF;
 }
-// One thread per (tile, group).  Every per-thread table the greedy indexes with a run-time slot / quarter lives
+// One thread per (tile, group).  Every per-thread table the greedy indexes with a run-time slot / class lives
 // in LDS (in registers such indexing compiles to scratch memory: 310-334 us per call on G22), and each thread
-// first copies its four rows into LDS (the first ST_CAP edges of each, independent loads), so the walk reads LDS;
+// first copies its eight rows into LDS (the first ST_CAP edges of each, independent loads), so the walk reads LDS;
 // rows longer than ST_CAP (hub vertices) read their tail from global memory.
 constexpr int ST_CAP = 64;
-constexpr int ST_THREADS = 64;
-constexpr int ST_LD = 17;  // ints per thread in the small tables (odd stride: no bank conflicts across threads)
+constexpr int ST_THREADS = 32;
+constexpr int ST_LD = 65;  // ints per thread in the class tables (odd stride: no bank conflicts across threads)
+constexpr int ST_SM = 33;
 __global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, SharedBufs sb) {
   if (sb.key[1] == 0ull) return;  // cached
-  __shared__ uint32_t rows[ST_THREADS][4][ST_CAP];
-  __shared__ int s_cnt[ST_THREADS * ST_LD], s_cur[ST_THREADS * ST_LD], s_small[ST_THREADS * ST_LD];
+  __shared__ uint32_t rows[ST_THREADS][8][ST_CAP];
+  __shared__ int s_cnt[ST_THREADS * ST_LD], s_cur[ST_THREADS * ST_LD], s_small[ST_THREADS * ST_SM];
   const int N = a.N;
   const int i = blockIdx.x * ST_THREADS + threadIdx.x;
-  const int t = i >> 2, g = i & 3;
+  const int t = i >> 1, g = i & 1;
   if (t >= sb.nt16) return;
   const int gid = a.gids[0];
   const int32_t* rp = a.gs.row_ptr + (size_t)gid * (N + 1);
@@ -273,15 +299,15 @@ __global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, Sh
   const int ml = (rp[n0 + 1] - rp[n0] + AG_UNROLL - 1) / AG_UNROLL * AG_UNROLL;
   if (g == 0) sb.tml[t] = ml;
   uint32_t (*my)[ST_CAP] = rows[threadIdx.x];
-  int* cnt = s_cnt + threadIdx.x * ST_LD;  // [slot j][quarter r] at 4j + r: edges of the quarter left
-  int* cur = s_cur + threadIdx.x * ST_LD;  // [j][r]: next position to scan for quarter r
-  int* bj = s_small + threadIdx.x * ST_LD;  // [0..3] row start, [4..7] ncls, [8..11] ord, [12..15] used
-  int* ncls = bj + 4;
-  int* ord = bj + 8;
-  int* used = bj + 12;
-  int k[4], len[4];
+  int* cnt = s_cnt + threadIdx.x * ST_LD;  // [slot j][class r] at 8j + r: edges of the class left
+  int* cur = s_cur + threadIdx.x * ST_LD;  // [j][r]: next position to scan for class r
+  int* bj = s_small + threadIdx.x * ST_SM;  // [0..7] row start, [8..15] ncls, [16..23] ord, [24..31] used
+  int* ncls = bj + 8;
+  int* ord = bj + 16;
+  int* used = bj + 24;
+  int k[8], len[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 8; ++j) {
     k[j] = sh_group_slot(g, j);
     const int slot = t * 16 + k[j];
     const bool valid = slot < N;
@@ -291,89 +317,168 @@ __global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, Sh
     sb.tn[slot] = valid ? n : -1;
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 8; ++j) {
     const int nl = min(len[j], ST_CAP);
     const int b = bj[j];
 #pragma unroll 8
     for (int e = 0; e < nl; ++e) my[j][e] = eg[b + e];
   }
   auto edge_at = [&](int j, int e) -> uint32_t { return e < ST_CAP ? my[j][e] : eg[bj[j] + e]; };
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    for (int e = 0; e < len[j]; ++e) {
-      const int r = edge_col(edge_at(j, e)) & 3;
-      c0 += r == 0; c1 += r == 1; c2 += r == 2; c3 += r == 3;
-    }
-    cnt[4 * j] = c0; cnt[4 * j + 1] = c1; cnt[4 * j + 2] = c2; cnt[4 * j + 3] = c3;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cur[4 * j + r] = 0;
+  for (int j = 0; j < 8; ++j) {
+    for (int r = 0; r < 8; ++r) cnt[8 * j + r] = cur[8 * j + r] = 0;
+    for (int e = 0; e < len[j]; ++e) ++cnt[8 * j + (edge_col(edge_at(j, e)) & 7)];
   }
   uint32_t* et = sb.et + (size_t)t * sb.MD * 16;
   for (int q = 0; q < max(ml, AG_UNROLL); ++q) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ncls[j] = (cnt[4 * j] > 0) + (cnt[4 * j + 1] > 0) + (cnt[4 * j + 2] > 0) + (cnt[4 * j + 3] > 0);
+    for (int j = 0; j < 8; ++j) {
+      int c = 0;
+      for (int r = 0; r < 8; ++r) c += cnt[8 * j + r] > 0;
+      ncls[j] = c;
       ord[j] = j;
       used[j] = 0;
     }
-    for (int x = 1; x < 4; ++x)  // insertion sort of the four slots by classes left (stable)
+    for (int x = 1; x < 8; ++x)  // insertion sort of the eight slots by classes left (stable)
       for (int y = x; y > 0 && ncls[ord[y]] < ncls[ord[y - 1]]; --y) {
         const int tmp = ord[y]; ord[y] = ord[y - 1]; ord[y - 1] = tmp;
       }
-    uint32_t word[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int x = 0; x < 8; ++x) {
       const int j = ord[x];
-      if (ncls[j] == 0) continue;
-      const int* cj = cnt + 4 * j;
-      int best = -1;
-      for (int r = 0; r < 4; ++r)  // a free quarter with the most edges left
-        if (cj[r] > 0 && used[r] == 0 && (best < 0 || cj[r] > cj[best])) best = r;
-      if (best < 0)
-        for (int r = 0; r < 4; ++r)  // else the least-used quarter (most edges left on ties)
-          if (cj[r] > 0 && (best < 0 || used[r] < used[best] || (used[r] == used[best] && cj[r] > cj[best])))
-            best = r;
-      ++used[best];
-      --cnt[4 * j + best];
-      int e = cur[4 * j + best];
-      uint32_t ex = edge_at(j, e);
-      while ((edge_col(ex) & 3) != best) ex = edge_at(j, ++e);
-      cur[4 * j + best] = e + 1;
-      // word of slot j (static register index: j == ord[x] is one of four values)
-      word[0] = j == 0 ? ex : word[0];
-      word[1] = j == 1 ? ex : word[1];
-      word[2] = j == 2 ? ex : word[2];
-      word[3] = j == 3 ? ex : word[3];
+      uint32_t ex = 0u;  // padding
+      if (ncls[j] > 0) {
+        const int* cj = cnt + 8 * j;
+        int best = -1;
+        for (int r = 0; r < 8; ++r)  // a free class with the most edges left
+          if (cj[r] > 0 && used[r] == 0 && (best < 0 || cj[r] > cj[best])) best = r;
+        if (best < 0)
+          for (int r = 0; r < 8; ++r)  // else the least-used class (most edges left on ties)
+            if (cj[r] > 0 && (best < 0 || used[r] < used[best] || (used[r] == used[best] && cj[r] > cj[best])))
+              best = r;
+        ++used[best];
+        --cnt[8 * j + best];
+        int e = cur[8 * j + best];
+        ex = edge_at(j, e);
+        while ((edge_col(ex) & 7) != best) ex = edge_at(j, ++e);
+        cur[8 * j + best] = e + 1;
+      }
+      et[((q >> 2) * 16 + sh_group_slot(g, j)) * 4 + (q & 3)] = ex;  // (no run-time index into k[])
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) et[((q >> 2) * 16 + k[j]) * 4 + (q & 3)] = word[j];
   }
 }
 
-// AG[item] (+)= A^(mode) . src[item] for the items = (slice, chunk, episode) blocks: an item's [N][16] block
-// of src sits in LDS while every node's neighbour sum is taken from it.  Persistent workgroups (one per CU)
-// walk items blockIdx.x, + grid, ...: the NEXT item's block is loaded into registers (8 float4 per thread)
-// while the current one is aggregated, then written to LDS between two barriers.  Lane = (node slot k =
-// lane >> 2 of a 16-node tile, feature quarter q = lane & 3); tiles of 16 nodes ranked by decreasing degree
-// walk their interleaved CSR rows (sb.et, bank-aware order) in lockstep, AG_TPW tiles per wave at a time, the next group of
-// AG_UNROLL edge words of each in flight (the loop is bound by the latency of these L2 reads: 16 waves x
-// 2 tiles x 4 words beat 8 waves x 2 x 8 and 8 x 2 x 16, 3.51 / 4.03 / 4.94 ms per configs[4] step);
-// each row is summed in the order of sb.et.
+// 16-bit form of an edge word for the packed table: the column (N <= 2048: 11 bits) | bit 14: +1 edge | bit 15: -1
+// edge (the shared path has +-1 weights; a padding word 0 is column 0 with weight 0)
+__device__ __forceinline__ uint16_t sh_w16(uint32_t ex) {
+  const int w = edge_w(ex);
+  return (uint16_t)(edge_col(ex) | (w > 0 ? 0x4000 : 0) | (w < 0 ? 0x8000 : 0));
+}
+// et -> et16 (rebuild calls only): tile t's first tml[t] x 16 interleaved words, tiles back to back (each a multiple
+// of 64 words: 128-B aligned), toff[t] its first word
+constexpr int SP_THREADS = 1024;
+__global__ __launch_bounds__(SP_THREADS) void shared_pack_kernel(SharedBufs sb) {
+  if (sb.key[1] == 0ull) return;  // cached
+  __shared__ int off[2049 / 16 + 2];
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int t = 0; t < sb.nt16; ++t) {
+      off[t] = o;
+      o += sb.tml[t] * 16;
+    }
+    off[sb.nt16] = o;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t <= sb.nt16; t += SP_THREADS) sb.toff[t] = off[t];
+  for (int t = 0; t < sb.nt16; ++t) {
+    const uint32_t* src = sb.et + (size_t)t * sb.MD * 16;
+    uint16_t* dst = sb.et16 + off[t];
+    const int n = sb.tml[t] * 16;
+    for (int i = threadIdx.x; i < n; i += SP_THREADS) dst[i] = sh_w16(src[i]);
+  }
+}
+
+// AG[item] (+)= A^(mode) . src[item] for the items = (slice, chunk, episode) blocks: an item's [N][8] block of src
+// sits in LDS while every node's neighbour sum is taken from it.  Persistent workgroups (one per CU) walk items
+// blockIdx.x, + grid, ...: the NEXT item's block is loaded into registers (4 float4 per thread) while the current
+// one is aggregated, then written to LDS between two barriers.  The packed edge table (et16) is copied into the LDS
+// behind the block once per workgroup when it fits (AG_LDS bytes in all), else read from L2.  Lane = (node slot
+// k = lane >> 1 of two 16-node tiles, feature half q = lane & 1); pairs of tiles ranked by decreasing degree (the
+// pair's first tile has the longer rows) walk their interleaved rows in lockstep, AG_TPW pairs per wave at a time,
+// the next 4 edge words of each read one step ahead; each row is summed in the order of et16.
 // mode 0: weight w (+-1); +1: edges with w > 0, weight 1; -1: edges with w < 0, weight 1.  accumulate: add
 // to AG (the A- pass of the edge phase).
 // XSRC 0: the block is read from src; 1 / 2 / 3: it is BUILT from the observation rows x (32 B per node) as
 // U = relu(Wx.x + w_a) / V = relu(Wx.x - w_a) / h0 = relu(W0.x) (mpnn.py:89-104, :55) with lin8_chunk: the
 // next item's x values are what is prefetched, the Linear runs when the block is written to LDS.
-constexpr int AG_PF = (8192 + 64 * AG_NW - 1) / (64 * AG_NW);  // float4 per thread per block: 128 KB (N <= 2048)
+constexpr int AG_LDS = 160 * 1024;                               // dynamic LDS of the aggregation launches
+constexpr int AG_PF = (4096 + 64 * AG_NW - 1) / (64 * AG_NW);  // float4 per thread per block: 64 KB (N <= 2048)
 constexpr int AG_XT = (2048 / 16 + AG_NW - 1) / AG_NW;          // 16-node x tiles per wave (N <= 2048)
+template <bool LDSW>
+__device__ __forceinline__ void sh_agg_item(const SharedBufs& sb, const float4* HL, const uint16_t* tab, float* dst,
+                                            int N, int mode, int accumulate, int w, int lane) {
+  const int k = lane >> 1, q = lane & 1;
+  const int jt = k >> 4, slot = k & 15;
+  typedef uint16_t __attribute__((ext_vector_type(4))) u16x4;
+  for (int p0 = w; 2 * p0 < sb.nt16; p0 += AG_TPW * AG_NW) {
+    int base[AG_TPW], ml[AG_TPW], mlw[AG_TPW], nd[AG_TPW];
+    u16x4 cur[AG_TPW], nxt[AG_TPW] = {};
+    float4 acc[AG_TPW];
+#pragma unroll
+    for (int j = 0; j < AG_TPW; ++j) {
+      const int p = p0 + j * AG_NW;
+      const int t = 2 * p + jt;
+      const bool live = 2 * p < sb.nt16 && t < sb.nt16;
+      ml[j] = live ? sb.tml[t] : 0;
+      mlw[j] = 2 * p < sb.nt16 ? uniform_i(sb.tml[2 * p]) : 0;  // the pair's longest rows (its first tile)
+      base[j] = (live ? sb.toff[t] : 0) + slot * 4;
+      nd[j] = live ? sb.tn[t * 16 + slot] : -1;
+      acc[j] = zero4();
+      cur[j] = ml[j] > 0 ? *reinterpret_cast<const u16x4*>(tab + base[j]) : u16x4{0, 0, 0, 0};
+    }
+    for (int i = 0; i < mlw[0]; i += 4) {
+#pragma unroll
+      for (int j = 0; j < AG_TPW; ++j) {
+        if (i + 4 < mlw[j]) {  // wave-uniform
+          const bool ok = i + 4 < ml[j];
+          const u16x4 v = *reinterpret_cast<const u16x4*>(tab + (ok ? base[j] + (i + 4) * 16 : 0));
+          nxt[j] = ok ? v : u16x4{0, 0, 0, 0};
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < AG_TPW; ++j) {
+        if (i < mlw[j]) {  // wave-uniform
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t w16 = cur[j][u];
+            const float pos = (float)((w16 >> 14) & 1u), neg = (float)(w16 >> 15);
+            const float f = mode == 0 ? pos - neg : (mode > 0 ? pos : neg);
+            const float4 h = HL[(w16 & 0x7FFu) * 2 + q];
+            acc[j].x = fmaf(f, h.x, acc[j].x); acc[j].y = fmaf(f, h.y, acc[j].y);
+            acc[j].z = fmaf(f, h.z, acc[j].z); acc[j].w = fmaf(f, h.w, acc[j].w);
+          }
+          cur[j] = nxt[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < AG_TPW; ++j) {
+      if (nd[j] >= 0) {
+        float* d = dst + (size_t)nd[j] * SH_FC + 4 * q;
+        float4 o = acc[j];
+        if (accumulate) {
+          const float4 pv = f4(d);
+          o = make_float4(pv.x + o.x, pv.y + o.y, pv.z + o.z, pv.w + o.w);
+        }
+        st4(d, o);
+      }
+    }
+  }
+}
 template <int XSRC>
 __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, SharedBufs sb, const float* src,
                                                                    int mode, int accumulate, int items) {
-  extern __shared__ __attribute__((aligned(16))) float4 HL[];  // [N][4]
+  extern __shared__ __attribute__((aligned(16))) float4 HL[];  // [N][2], then the packed edge table
   const int N = a.N;
   if (mode < 0 && !(a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0)) return;  // no -1 edge: A- . V = 0
-  const int n4 = N * 4;
+  const int n2 = N * 2;
   constexpr int NPF = XSRC ? 1 : AG_PF;
   constexpr int NXT = XSRC ? AG_XT : 1;
   float4 pf[NPF];
@@ -382,14 +487,14 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
   const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
   auto load_block = [&](int it) {
     if (XSRC == 0) {
-      const float* S = src + (size_t)it * N * 16;
+      const float* S = src + (size_t)it * N * SH_FC;
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
         const int i = threadIdx.x + u * 64 * AG_NW;
-        pf[u] = f4_nt(S + 4 * (size_t)min(i, n4 - 1));
+        pf[u] = f4_nt(S + 4 * (size_t)min(i, n2 - 1));
       }
     } else {
-      const int e = it % SH_EPS, c = (it / SH_EPS) % 4, s = it / (4 * SH_EPS);
+      const int e = it % SH_EPS, c = (it / SH_EPS) % 8, s = it / (8 * SH_EPS);
       const int ep = s * SH_EPS + e;
       pc = c;
 #pragma unroll
@@ -406,113 +511,45 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
         const int i = threadIdx.x + u * 64 * AG_NW;
-        if (i < n4) HL[i] = pf[u];
+        if (i < n2) HL[i] = pf[u];
       }
     } else {
-      const float4 wa = f4(a.P + PK_WA + 16 * pc + 4 * (ln >> 4));
+      // lin8_chunk gives features 16 (pc / 2) + 4 (ln >> 4) ..: the lanes of 8-feature chunk pc keep theirs
+      const float4 wa = f4(a.P + PK_WA + 16 * (pc >> 1) + 4 * (ln >> 4));
+      const bool mine = (ln >> 5) == (pc & 1);
 #pragma unroll
       for (int j = 0; j < NXT; ++j) {
         const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
         if ((wv_ + j * AG_NW) * 16 >= N) break;  // wave-uniform: MFMAs below run with EXEC all ones
-        const f32x4 z = lin8_chunk(a.P + (XSRC == 3 ? PK_W0 : PK_WX), pc, xk0[j], xk1[j], ln);
+        const f32x4 z = lin8_chunk(a.P + (XSRC == 3 ? PK_W0 : PK_WX), pc >> 1, xk0[j], xk1[j], ln);
         const float sg = XSRC == 2 ? -1.f : 1.f;
         float4 v = XSRC == 3 ? relu4(z)
                              : make_float4(relu(fmaf(sg, wa.x, z[0])), relu(fmaf(sg, wa.y, z[1])),
                                            relu(fmaf(sg, wa.z, z[2])), relu(fmaf(sg, wa.w, z[3])));
-        if (n < N) HL[n * 4 + (ln >> 4)] = v;  // padding episodes (x = 0) only ever reach their own rows
+        if (mine && n < N) HL[n * 2 + ((ln >> 4) & 1)] = v;  // padding episodes (x = 0) only reach their own rows
       }
     }
   };
   int item = blockIdx.x;
   if (item >= items) return;
+  const int nwords = sb.toff[sb.nt16];
+  const bool in_lds = (size_t)n2 * 16 + (size_t)nwords * 2 <= (size_t)AG_LDS;  // uniform
+  uint16_t* T16 = reinterpret_cast<uint16_t*>(HL + n2);                         // 16-B aligned
+  if (in_lds) {
+    const uint4* s4p = reinterpret_cast<const uint4*>(sb.et16);
+    uint4* d4p = reinterpret_cast<uint4*>(T16);
+    for (int i = threadIdx.x; i < nwords / 8; i += 64 * AG_NW) d4p[i] = s4p[i];  // nwords: a multiple of 64
+  }
   load_block(item);
   store_block();
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int k = lane >> 2, q = lane & 3;
-  // edges i .. i + AG_UNROLL - 1 of a slot: AG_UNROLL / 4 16-B loads (i a multiple of 4)
-  auto load_group = [](const uint32_t* e, int i, uint32_t(&dst)[AG_UNROLL]) {
-#pragma unroll
-    for (int g = 0; g < AG_UNROLL / 4; ++g) {
-      const uint4 v = *reinterpret_cast<const uint4*>(e + ((i >> 2) + g) * 64);
-      dst[4 * g] = v.x; dst[4 * g + 1] = v.y; dst[4 * g + 2] = v.z; dst[4 * g + 3] = v.w;
-    }
-  };
   for (; item < items; item += gridDim.x) {
     const bool more = item + (int)gridDim.x < items;
     if (more) load_block(item + gridDim.x);  // lands while this item is aggregated
-    float* dst = sb.AG + (size_t)item * N * 16;
-    for (int tb = w; tb < sb.nt16; tb += AG_TPW * AG_NW) {
-      // AG_TPW tiles tb, tb + AG_NW, ... at once (ranked by decreasing degree: the first is the longest)
-      const uint32_t* et[AG_TPW];
-      uint32_t cur[AG_TPW][AG_UNROLL], nxt[AG_TPW][AG_UNROLL];
-#if AG_DEPTH2
-      uint32_t nx2[AG_TPW][AG_UNROLL];
-#endif
-      int nd[AG_TPW], ml[AG_TPW];
-      float4 acc[AG_TPW];
-#pragma unroll
-      for (int j = 0; j < AG_TPW; ++j) {
-        const int t = tb + j * AG_NW;
-        const bool live = t < sb.nt16;  // wave-uniform
-        et[j] = sb.et + (size_t)(live ? t : tb) * sb.MD * 16 + 4 * k;  // slot k's groups, 64 words apart
-        load_group(et[j], 0, cur[j]);
-        nd[j] = live ? sb.tn[t * 16 + k] : -1;
-        ml[j] = live ? uniform_i(sb.tml[t]) : 0;
-        acc[j] = zero4();
-#if AG_DEPTH2
-        if (AG_UNROLL < ml[j]) {
-          load_group(et[j], AG_UNROLL, nxt[j]);
-        }
-#endif
-      }
-      for (int i = 0; i < ml[0]; i += AG_UNROLL) {
-#pragma unroll
-        for (int j = 0; j < AG_TPW; ++j) {
-#if AG_DEPTH2
-          if (i + 2 * AG_UNROLL < ml[j]) {
-            load_group(et[j], i + 2 * AG_UNROLL, nx2[j]);  // two groups ahead
-          }
-#else
-          if (i + AG_UNROLL < ml[j]) {
-            load_group(et[j], i + AG_UNROLL, nxt[j]);  // next group in flight
-          }
-#endif
-        }
-#pragma unroll
-        for (int j = 0; j < AG_TPW; ++j) {
-          if (i < ml[j]) {
-#pragma unroll
-            for (int u = 0; u < AG_UNROLL; ++u) {
-              const int wv = edge_w(cur[j][u]);
-              const float f = mode == 0 ? (float)wv : mode > 0 ? (wv > 0 ? 1.f : 0.f) : (wv < 0 ? 1.f : 0.f);
-              const float4 h = HL[edge_col(cur[j][u]) * 4 + q];
-              acc[j].x = fmaf(f, h.x, acc[j].x); acc[j].y = fmaf(f, h.y, acc[j].y);
-              acc[j].z = fmaf(f, h.z, acc[j].z); acc[j].w = fmaf(f, h.w, acc[j].w);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < AG_UNROLL; ++u) {
-            cur[j][u] = nxt[j][u];
-#if AG_DEPTH2
-            nxt[j][u] = nx2[j][u];
-#endif
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < AG_TPW; ++j) {
-        if (nd[j] >= 0) {
-          float* d = dst + (size_t)nd[j] * 16 + 4 * q;
-          float4 o = acc[j];
-          if (accumulate) {
-            const float4 p = f4(d);
-            o = make_float4(p.x + o.x, p.y + o.y, p.z + o.z, p.w + o.w);
-          }
-          st4(d, o);
-        }
-      }
-    }
+    float* dst = sb.AG + (size_t)item * N * SH_FC;
+    if (in_lds) sh_agg_item<true>(sb, HL, T16, dst, N, mode, accumulate, w, lane);
+    else sh_agg_item<false>(sb, HL, sb.et16, dst, N, mode, accumulate, w, lane);
     __syncthreads();  // every wave is done with this block
     if (more) store_block();
     __syncthreads();
@@ -527,14 +564,20 @@ template <int PHASE>
 __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, SharedBufs sb, int layer,
                                                                    const float* Hc, float* Hn) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  uint16_t* WL = reinterpret_cast<uint16_t*>(lds);  // Wf (24 fragments) or Wm, Wu (96 fragments)
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int c16 = lane & 15, s4 = lane >> 4;
   const int kn = c16 / SH_EPS, eps = c16 % SH_EPS;
+  uint16_t* WL = reinterpret_cast<uint16_t*>(lds);
+#if ECO_AB_SHARED_BF3  // A/B builds only: the six-product bf16x3 Linears (Wf 24 fragments, Wm + Wu 96)
   const uint16_t* PB = reinterpret_cast<const uint16_t*>(a.P + PK_BF);
   if (PHASE == 0) glds_frags<SH_NW>(WL, PB + BF_WF, 24, w, lane);
   else glds_frags<SH_NW>(WL, PB + BF_LAYER + layer * BF_LAYER_STRIDE, 96, w, lane);
+#else  // fp16x2 pieces (PK_FH): Wf 16 fragments, Wm + Wu of the layer 64 (four 64-input halves)
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(a.P + PK_FH);
+  if (PHASE == 0) glds_frags<SH_NW>(WL, PH + FH_WF, 16, w, lane);
+  else glds_frags<SH_NW>(WL, PH + FH_LAYER + layer * FH_LAYER_STRIDE, 64, w, lane);
+#endif
   const int N = a.N;
   const int gid = a.gids[0];
   const float* P = a.P;
@@ -603,7 +646,13 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#if ECO_AB_SHARED_BF3
       mm_bf3_seq(d, acc, WL, lane);
+#else
+      const int kx = node_exp<4>(acc);
+      mm_fh_seq(d, acc, exp2i(kx), WL, lane);
+      unscale(d, kx + fh_kw(P, 0));
+#endif
       if (nvalid) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) st4_nt(sb.EB + ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
@@ -612,25 +661,46 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#if ECO_AB_SHARED_BF3
       mm_bf3_seq(d, acc, WL, lane);               // message = relu(Wm . [agg, e])
       mm_bf3_seq(d, cu.ev, WL + BF_HALF, lane);
+#else
+      {  // message = relu(Wm . [agg, e]): one node scale over both halves, as the dense kernels
+        const int kx = node_exp2(acc, cu.ev);
+        const float sf = exp2i(kx);
+        mm_fh_seq(d, cu.ev, sf, WL + FH_HALF, lane);
+        mm_fh_seq(d, acc, sf, WL, lane);
+        unscale(d, kx + fh_kw(P, 1 + 2 * layer));
+      }
+#endif
       float4 mr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) mr[c] = relu4(d[c]);
       f32x4 hn[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float4 hc[4];
       if (Hc) {
-        mm_bf3_seq(hn, cu.hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hc[c] = cu.hc[c];
       } else {  // layer 0: h0 = relu(W0 . x) of this lane's row (lin8, as the aggregation built it)
         f32x4 z[4];
         lin8(z, P + PK_W0, cu.xk0, cu.xk1, lane);
-        float4 hc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) hc[c] = relu4(z[c]);
-        mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);
       }
+#if ECO_AB_SHARED_BF3
+      mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
       mm_bf3_seq(hn, mr, WL + 3 * BF_HALF, lane);
+#else
+      {  // h' = relu(Wu . [h, m])
+        const int kx = node_exp2(hc, mr);
+        const float sf = exp2i(kx);
+        mm_fh_seq(hn, hc, sf, WL + 2 * FH_HALF, lane);
+        mm_fh_seq(hn, mr, sf, WL + 3 * FH_HALF, lane);
+        unscale(hn, kx + fh_kw(P, 2 + 2 * layer));
+      }
+#endif
       if (PHASE == 1) {
         if (nvalid) {
 #pragma unroll
@@ -757,16 +827,21 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
 #endif
   shared_key_kernel<<<1, SK_THREADS, 0, st>>>(a, key);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
-  shared_tiles_kernel<<<(sb.nt16 * 4 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
-  const int items = sb.S * 4 * SH_EPS;  // (slice, chunk, episode) blocks
+  shared_tiles_kernel<<<(sb.nt16 * 2 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
+  shared_pack_kernel<<<1, SP_THREADS, 0, st>>>(sb);
+  const int items = sb.S * 8 * SH_EPS;  // (slice, chunk, episode) blocks
   const int agrid = std::min(items, shared_grid());
-  const size_t lds_agg = (size_t)a.N * 64;
+  const size_t lds_agg = AG_LDS;
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   const int grid = shared_grid();
+#if ECO_AB_SHARED_BF3
   const size_t lds_edge = 24 * BF_FRAG * 2, lds_layer = 96 * BF_FRAG * 2;
+#else
+  const size_t lds_edge = 16 * FH_FRAG * 2, lds_layer = 64 * FH_FRAG * 2;
+#endif
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_edge);
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -49,7 +49,7 @@ class DQN:
                  network_save_path='network', evaluate=True, test_envs=None, test_episodes=20,
                  test_frequency=10000, test_save_path='test_scores', test_metric=TestMetric.ENERGY_ERROR,
                  logging=True, seed=None, train_minibatch=None, graph_pool_ids=None, regenerate_graphs=None,
-                 compact_replay=None, target_sync="grad_steps"):
+                 compact_replay=None, target_sync="grad_steps", overlap_evaluation=True):
         if isinstance(envs, (list, tuple)):
             if len(envs) != 1:
                 raise NotImplementedError("pass one VecSpinSystem (it already holds B episodes)")
@@ -93,6 +93,8 @@ class DQN:
 
         self.network = network()
         self.target_network = network()
+        self._network_factory = network
+        self._eval_net = None
         if init_network_params is not None:
             self.load(init_network_params)
         elif init_weight_std is not None:
@@ -174,6 +176,10 @@ class DQN:
         self.test_metric = test_metric
         self.save_network_frequency = save_network_frequency
         self.network_save_path = network_save_path
+        # learn(): evaluations that take the one-fill path run on a side stream on a snapshot of the weights while
+        # training continues (same results: the snapshot is the network at the evaluation's timestep)
+        self.overlap_evaluation = overlap_evaluation
+        self._eval_stream = None
 
         self._act_counter = 0
         self._alloc_train_buffers(self.M)
@@ -446,6 +452,21 @@ class DQN:
         self.start()
         rank = torch.distributed.get_rank() if self.dist else 0
         test_scores, test_solutions = [], []
+        pending = None  # an overlapped evaluation in flight
+
+        def record(tk, test_score, test_solution, net):
+            if verbose and rank == 0:
+                print('\nTest score: {}\nTest solution: {}\n'.format(np.round(test_score, 3),
+                                                                    np.round(test_solution, 3)))
+            if all(test_score > sc for _, sc in test_scores) and rank == 0:
+                main, ext = os.path.splitext(self.network_save_path)
+                self.save(main + "_best" + (ext or ".pth"), network=net)
+            test_scores.append([tk, test_score])
+            test_solutions.append([tk, test_solution])
+
+        def finish(p):
+            record(p["tk"], *self._eval_one_fill_finish(p), p["net"])
+
         while self._timestep < timesteps:
             t_prev = self._timestep
             self.iteration()
@@ -459,21 +480,24 @@ class DQN:
                 # graphs regenerated with check=False since the last sync point: an edge-slot overflow
                 # sets the device error word (the slot becomes an empty graph); surface it here
                 self.graphs.check_errors()
+            if pending is not None and pending["done"].query():
+                finish(pending)
+                pending = None
             if self.evaluate and crossed_test:
                 tk = (t // self.test_frequency) * self.test_frequency
-                test_score, test_solution = self.evaluate_agent()
-                if verbose and rank == 0:
-                    print('\nTest score: {}\nTest solution: {}\n'.format(np.round(test_score, 3),
-                                                                        np.round(test_solution, 3)))
-                if all(test_score > sc for _, sc in test_scores) and rank == 0:
-                    main, ext = os.path.splitext(self.network_save_path)
-                    self.save(main + "_best" + (ext or ".pth"))
-                test_scores.append([tk, test_score])
-                test_solutions.append([tk, test_solution])
+                if pending is not None:  # one evaluation in flight at a time (its snapshot is reused)
+                    finish(pending)
+                    pending = None
+                if self.overlap_evaluation and self._one_fill_ok(self._test_env(), None):
+                    pending = self._evaluate_overlapped(tk)
+                else:
+                    record(tk, *self.evaluate_agent(), self.network)
             if t // self.save_network_frequency > t_prev // self.save_network_frequency and rank == 0:
                 tk = (t // self.save_network_frequency) * self.save_network_frequency
                 main, ext = os.path.splitext(self.network_save_path)
                 self.save(main + str(tk) + (ext or ".pth"))
+        if pending is not None:
+            finish(pending)
         if self.regenerate_graphs is not None:
             self.graphs.check_errors()
         losses = self.losses()
@@ -515,17 +539,14 @@ class DQN:
           CUMULATIVE_REWARD -> (sum of rewards, 0)          (:560-561, :580-581)
           ENERGY_ERROR      -> (0, 0), as in the reference whose branch is commented out (:571-583)
         Returns (mean score, mean solution)."""
-        env = test_env or self.test_envs
-        if env is None:
-            # dqn.py:225-227: test on the training environment(s) -- here a separate batch of episodes
-            # over the training graph pool (the training episodes keep running untouched)
-            from ...envs.batched import VecSpinSystem
-            env = self.test_envs = VecSpinSystem(self.graphs, max(1, int(batch_size or self.minibatch_size)),
-                                                 self.env.max_steps, **self.env.env_args)
-        if isinstance(env, (list, tuple)):
-            env = env[0]
+        env = self._test_env(test_env, batch_size)
         slots = min(int(batch_size or self.minibatch_size), env.n_envs)
         dev = self.device
+        act_cfg = self._act_config(0.0)
+        act_cfg.reversible = int(env.reversible_spins)
+        act_cfg.allowed_value = float(env.allowed_action_value())
+        if self._one_fill_ok(env, batch_size):
+            return self._eval_one_fill_finish(self._eval_one_fill_launch(env, act_cfg, self.network))
         if not hasattr(env, "_eval_next_graph"):
             env._eval_next_graph = 0
         n_graphs = env.graphs.n_graphs
@@ -537,11 +558,6 @@ class DQN:
         scores, solutions = [], []
         started = 0
         metric = self.test_metric
-        act_cfg = self._act_config(0.0)
-        act_cfg.reversible = int(env.reversible_spins)
-        act_cfg.allowed_value = float(env.allowed_action_value())
-        if self.test_episodes <= slots and env.reversible_spins and env.cfg.stopping == 1:
-            return self._evaluate_one_fill(env, act_cfg, metric)
         while len(scores) < self.test_episodes:
             free = (~active[:slots]).nonzero().flatten().cpu().numpy()
             take = free[:max(0, self.test_episodes - started)]
@@ -589,17 +605,37 @@ class DQN:
         self.last_evaluation = (scores, solutions)  # per episode, in completion order
         return float(np.mean(scores)), float(np.mean(solutions))
 
-    def _evaluate_one_fill(self, env, act_cfg, metric):
+    def _test_env(self, test_env=None, batch_size=None):
+        env = test_env or self.test_envs
+        if env is None:
+            # dqn.py:225-227: test on the training environment(s) -- here a separate batch of episodes
+            # over the training graph pool (the training episodes keep running untouched)
+            from ...envs.batched import VecSpinSystem
+            env = self.test_envs = VecSpinSystem(self.graphs, max(1, int(batch_size or self.minibatch_size)),
+                                                 self.env.max_steps, **self.env.env_args)
+        if isinstance(env, (list, tuple)):
+            env = env[0]
+        return env
+
+    def _one_fill_ok(self, env, batch_size):
+        """Every test episode fits the slots at once and ends exactly at max_steps (reversible spins,
+        Stopping.NORMAL, spinsystem.py:539-554)."""
+        slots = min(int(batch_size or self.minibatch_size), env.n_envs)
+        return self.test_episodes <= slots and env.reversible_spins and env.cfg.stopping == 1
+
+    def _eval_one_fill_launch(self, env, act_cfg, net):
         """evaluate_agent when every test episode fits the slots at once (the reference's 50 ER-200 test graphs
-        in 64 slots) and every episode ends exactly at max_steps (reversible spins, Stopping.NORMAL,
-        spinsystem.py:539-554): the same resets, predictions and steps as the refill loop, with no host
-        synchronisation per step.  The k episodes take slots 0..k-1, so each prediction's batch (its norm.max()
-        coupling, dqn.py:546-547) is the contiguous prefix obs_x[:k] -- all of them are active until the last
-        step, as in the refill loop -- and the env is read once at the end.  Scores are listed in completion
-        order (end step, then slot), as the refill loop appends them."""
+        in 64 slots) and every episode ends exactly at max_steps: the same resets, predictions and steps as the
+        refill loop, issued with no host synchronisation (on the current stream).  The k episodes take slots
+        0..k-1, so each prediction's batch (its norm.max() coupling, dqn.py:546-547) is the contiguous prefix
+        obs_x[:k] -- all of them are active until the last step, as in the refill loop."""
         dev = self.device
         k = self.test_episodes
         n_graphs = env.graphs.n_graphs
+        if not hasattr(env, "_eval_next_graph"):
+            env._eval_next_graph = 0
+        # every slot holds a valid episode (unused ones run to their end and stay masked), as evaluate_agent
+        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.seed)
         mask = np.zeros(env.n_envs, dtype=np.uint8)
         mask[:k] = 1
         gids = np.zeros(env.n_envs, dtype=np.int64)
@@ -611,11 +647,19 @@ class DQN:
         sub = acts[:k]
         act_cfg.counter = 0
         for _ in range(env.max_steps):
-            self.network.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=_lib.ECO_NORM_PER_CALL,
-                                        act=act_cfg, actions_out=sub)
+            net.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=_lib.ECO_NORM_PER_CALL,
+                               act=act_cfg, actions_out=sub)
             _, rew, _ = env.step(acts)
             cum += rew
-        st = env.read()
+        st = env.read()  # device scalars; read by _eval_one_fill_finish
+        return {"env": env, "k": k, "cum": cum, "st": st, "metric": self.test_metric}
+
+    def _eval_one_fill_finish(self, p):
+        """Scores of a launched one-fill evaluation, listed in completion order (end step, then slot), as the
+        refill loop appends them."""
+        env, k, cum, st, metric = p["env"], p["k"], p["cum"], p["st"], p["metric"]
+        if p.get("done") is not None:
+            p["done"].synchronize()
         ends = st["current_step"][:k].cpu().numpy()
         order = np.lexsort((np.arange(k), ends))
         scores, solutions = [], []
@@ -636,6 +680,33 @@ class DQN:
         self.last_evaluation = (scores, solutions)
         return float(np.mean(scores)), float(np.mean(solutions))
 
+    @torch.no_grad()
+    def _evaluate_overlapped(self, tk):
+        """learn()'s evaluation at timestep tk without stopping training: the online weights are copied into a
+        snapshot network on the training stream, and the one-fill evaluation runs on a side stream that waits
+        for that copy only; training kernels keep going.  The evaluation's kernels and inputs are those of
+        evaluate_agent() at tk, so its scores are identical; learn() records them (and saves the snapshot as
+        `_best`) once the side stream's completion event has fired, or at the next evaluation / the end."""
+        if self._eval_net is None:
+            self._eval_net = self._network_factory()
+        if self._eval_stream is None:
+            self._eval_stream = torch.cuda.Stream(device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        self._eval_net.flat.copy_(self.network.flat)
+        snap = torch.cuda.Event()
+        snap.record(main)
+        env = self._test_env()
+        act_cfg = self._act_config(0.0)
+        act_cfg.reversible = int(env.reversible_spins)
+        act_cfg.allowed_value = float(env.allowed_action_value())
+        with torch.cuda.stream(self._eval_stream):
+            self._eval_stream.wait_event(snap)
+            p = self._eval_one_fill_launch(env, act_cfg, self._eval_net)
+            p["done"] = torch.cuda.Event()
+            p["done"].record(self._eval_stream)
+        p["tk"], p["net"] = tk, self._eval_net
+        return p
+
     @staticmethod
     def _final_solution(env, st, i):
         """scorer.get_solution of the episode's current spins (score_solver.py:263-271, 377-381,
@@ -653,10 +724,12 @@ class DQN:
         return 0.0 if invalid else size
 
     # ------------------------------------------------------------ checkpoint
-    def save(self, path='network.pth'):
+    def save(self, path='network.pth', network=None):
         """dqn.py:604-607: torch.save(state_dict) -- loadable by the reference MPNN.  The reference's
-        extension fix-up is a no-op expression (`path + '.pth'`, :606), so `path` is used as given."""
-        torch.save({k: v.detach().cpu().clone() for k, v in self.network.state_dict().items()}, path)
+        extension fix-up is a no-op expression (`path + '.pth'`, :606), so `path` is used as given.
+        network: another network to save (learn()'s evaluation snapshot); default the online network."""
+        net = self.network if network is None else network
+        torch.save({k: v.detach().cpu().clone() for k, v in net.state_dict().items()}, path)
 
     def load(self, path):
         """dqn.py:609-610 (weights_only: state_dicts are plain tensors)."""

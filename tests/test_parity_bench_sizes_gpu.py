@@ -367,6 +367,40 @@ def test_shared_graph_forward_matches_per_episode_and_oracle(weights):
             assert torch.equal(a, masked.argmax(1))
 
 
+def test_shared_graph_forward_edge_table_beyond_lds():
+    """Shared-graph path on a graph whose packed 16-bit edge table does NOT fit the aggregation's LDS next to the
+    [N][8] block (ER(1500, 0.06): ~135k words = 270 KB; eco_mpnn_shared.h reads it from L2 then), +-1 weights, B = 9
+    (two full slices and a padded one): against the per-episode kernel on the replicated graph and the oracle."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip._lib import ECO_NORM_PER_CALL
+    n, B = 1500, 9
+    rng = np.random.default_rng(1500)
+    J = og.er_graph(n, 0.06, rng, weights="discrete")
+    assert int((J != 0).sum()) * 2 > 160 * 1024 - n * 32  # the table cannot sit in the LDS
+    one = GraphStore.from_dense([J])
+    rep = GraphStore.from_dense([J] * B)
+    g = torch.Generator().manual_seed(8)
+    wts = mo.init_weights(g, std=0.1)
+    net = MPNN(device="cuda")
+    net.load_state_dict(wts)
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    q1 = net.forward_graphs(xc, one, torch.zeros(B, dtype=torch.int32, device="cuda"), norm_scope=ECO_NORM_PER_CALL)
+    qr = net.forward_graphs(xc, rep, torch.arange(B, dtype=torch.int32, device="cuda"), norm_scope=ECO_NORM_PER_CALL)
+    assert torch.isfinite(q1).all()
+    err = float(((q1 - qr).abs() / (1 + qr.abs())).max())
+    assert err <= 5e-5, err
+    wc = {k: v.cuda() for k, v in wts.items()}
+    adj = torch.from_numpy(J).float().cuda().unsqueeze(0)
+    for b in (0, 8):
+        with torch.no_grad():
+            ref = mo.forward(wc, _obs(xc[b:b + 1], adj))
+        assert float(((q1[b] - ref).abs() / (1 + ref.abs())).max()) <= 5e-5, b
+
+
 def test_shared_graph_forward_hub_and_isolated_nodes():
     """Shared-graph path on a graph with a hub adjacent to every other vertex (one CSR row of N - 1 edges: the
     longest aggregation tile row) and isolated vertices (empty rows, norm clamped to 1), +-1 weights, B = 6
