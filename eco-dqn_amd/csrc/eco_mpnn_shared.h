@@ -37,6 +37,9 @@ namespace eco {
 #ifndef SH_NW_X
 #define SH_NW_X 16
 #endif
+#ifndef ECO_AB_XBUILD
+#define ECO_AB_XBUILD 0                // A/B timing probes only (wrong results): 1 no MFMA in the x build, 2 no x loads
+#endif
 #ifndef ECO_AB_SHARED_BF3
 #define ECO_AB_SHARED_BF3 0            // A/B builds only (tools/): the round-3 six-product bf16x3 Linears
 #endif
@@ -74,7 +77,7 @@ struct SharedBufs {
   uint16_t* et16; // the same words packed (tile t from toff[t], tml[t] x 16 words each) as sh_w16
   int32_t* toff;  // [nt16 + 1] first 16-bit word of each tile in et16; toff[nt16] = the table's words
   const uint64_t* key;  // workspace header: [0] key of the cached perm / tile tables, [1] 1 = rebuild this call
-  int Epad, S, ntiles, nt16, MD;
+  int Epad, S, ntiles, nt16, MD, N;
 };
 
 inline int shared_grid() {  // persistent Linear workgroups: one per CU
@@ -101,6 +104,7 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   SharedBufs sb;
   sb.S = (B + SH_EPS - 1) / SH_EPS;
   sb.Epad = sb.S * SH_EPS;
+  sb.N = N;
   sb.ntiles = (N + SH_NPT - 1) / SH_NPT;
   const size_t T1 = (size_t)N * sb.Epad * 64;
   sb.HA = base;
@@ -365,15 +369,19 @@ __global__ __launch_bounds__(ST_THREADS) void shared_tiles_kernel(MpnnArgs a, Sh
   }
 }
 
-// 16-bit form of an edge word for the packed table: the column (N <= 2048: 11 bits) | bit 14: +1 edge | bit 15: -1
-// edge (the shared path has +-1 weights; a padding word 0 is column 0 with weight 0)
-__device__ __forceinline__ uint16_t sh_w16(uint32_t ex) {
+// 16-bit form of an edge word for the packed table: the byte offset of the column's 32-B block row (col x 32, N <=
+// 2048: bits 5..15) | the weight as a 2-bit signed field in bits 0..1 (+1: 01, -1: 11; the shared path has +-1
+// weights).  A padding word (et word 0) has weight 0 and points at row N, which the aggregation keeps zero in its
+// LDS block (N < 2048; row 0 at N = 2048): graphs without -1 edges then sum every word with weight 1.
+__device__ __forceinline__ uint16_t sh_w16(uint32_t ex, int N) {
+  if (ex == 0u) return (uint16_t)(N < 2048 ? N << 5 : 0);
   const int w = edge_w(ex);
-  return (uint16_t)(edge_col(ex) | (w > 0 ? 0x4000 : 0) | (w < 0 ? 0x8000 : 0));
+  return (uint16_t)((edge_col(ex) << 5) | (w > 0 ? 1 : (w < 0 ? 3 : 0)));
 }
 // et -> et16 (rebuild calls only): tile t's first tml[t] x 16 interleaved words, tiles back to back (each a multiple
 // of 64 words: 128-B aligned), toff[t] its first word
 constexpr int SP_THREADS = 1024;
+constexpr int AG_ZW = 64;  // zero words behind the packed table
 __global__ __launch_bounds__(SP_THREADS) void shared_pack_kernel(SharedBufs sb) {
   if (sb.key[1] == 0ull) return;  // cached
   __shared__ int off[2049 / 16 + 2];
@@ -391,8 +399,10 @@ __global__ __launch_bounds__(SP_THREADS) void shared_pack_kernel(SharedBufs sb) 
     const uint32_t* src = sb.et + (size_t)t * sb.MD * 16;
     uint16_t* dst = sb.et16 + off[t];
     const int n = sb.tml[t] * 16;
-    for (int i = threadIdx.x; i < n; i += SP_THREADS) dst[i] = sh_w16(src[i]);
+    for (int i = threadIdx.x; i < n; i += SP_THREADS) dst[i] = sh_w16(src[i], sb.N);
   }
+  // 64 zero words behind the table: the reads of a lane past its row (and of padding pairs) point there
+  for (int i = threadIdx.x; i < AG_ZW; i += SP_THREADS) sb.et16[off[sb.nt16] + i] = sh_w16(0u, sb.N);
 }
 
 // AG[item] (+)= A^(mode) . src[item] for the items = (slice, chunk, episode) blocks: an item's [N][8] block of src
@@ -409,60 +419,108 @@ __global__ __launch_bounds__(SP_THREADS) void shared_pack_kernel(SharedBufs sb) 
 // U = relu(Wx.x + w_a) / V = relu(Wx.x - w_a) / h0 = relu(W0.x) (mpnn.py:89-104, :55) with lin8_chunk: the
 // next item's x values are what is prefetched, the Linear runs when the block is written to LDS.
 constexpr int AG_LDS = 160 * 1024;                               // dynamic LDS of the aggregation launches
+constexpr int AG_WL = 576;                                        // floats of the x-build weights (64 x 8 + 64)
 constexpr int AG_PF = (4096 + 64 * AG_NW - 1) / (64 * AG_NW);  // float4 per thread per block: 64 KB (N <= 2048)
 constexpr int AG_XT = (2048 / 16 + AG_NW - 1) / AG_NW;          // 16-node x tiles per wave (N <= 2048)
-template <bool LDSW>
-__device__ __forceinline__ void sh_agg_item(const SharedBufs& sb, const float4* HL, const uint16_t* tab, float* dst,
-                                            int N, int mode, int accumulate, int w, int lane) {
-  const int k = lane >> 1, q = lane & 1;
+// A wave's tile pairs are the same for every item: p = w + (r AG_TPW + j) AG_NW, rounds r < AG_R.  Their row
+// lengths, table offsets and output nodes are read once per workgroup into registers (global loads inside the item
+// loop would wait for the next block's prefetch too: vmcnt counts in order).
+constexpr int AG_R = (2048 / 32 + AG_TPW * AG_NW - 1) / (AG_TPW * AG_NW);
+struct AgPairs {
+  int base[AG_R][AG_TPW], ml[AG_R][AG_TPW], mlw[AG_R][AG_TPW], nd[AG_R][AG_TPW];
+};
+__device__ __forceinline__ void sh_agg_pairs(const SharedBufs& sb, AgPairs& P, int w, int lane) {
+  const int k = lane >> 1;
   const int jt = k >> 4, slot = k & 15;
-  typedef uint16_t __attribute__((ext_vector_type(4))) u16x4;
-  for (int p0 = w; 2 * p0 < sb.nt16; p0 += AG_TPW * AG_NW) {
-    int base[AG_TPW], ml[AG_TPW], mlw[AG_TPW], nd[AG_TPW];
-    u16x4 cur[AG_TPW], nxt[AG_TPW] = {};
-    float4 acc[AG_TPW];
+#pragma unroll
+  for (int r = 0; r < AG_R; ++r)
 #pragma unroll
     for (int j = 0; j < AG_TPW; ++j) {
-      const int p = p0 + j * AG_NW;
+      const int p = w + (r * AG_TPW + j) * AG_NW;
       const int t = 2 * p + jt;
       const bool live = 2 * p < sb.nt16 && t < sb.nt16;
-      ml[j] = live ? sb.tml[t] : 0;
-      mlw[j] = 2 * p < sb.nt16 ? uniform_i(sb.tml[2 * p]) : 0;  // the pair's longest rows (its first tile)
-      base[j] = (live ? sb.toff[t] : 0) + slot * 4;
-      nd[j] = live ? sb.tn[t * 16 + slot] : -1;
-      acc[j] = zero4();
-      cur[j] = ml[j] > 0 ? *reinterpret_cast<const u16x4*>(tab + base[j]) : u16x4{0, 0, 0, 0};
+      P.ml[r][j] = live ? sb.tml[t] : 0;
+      P.mlw[r][j] = 2 * p < sb.nt16 ? uniform_i(sb.tml[2 * p]) : 0;  // the pair's longest rows (its first tile)
+      P.base[r][j] = (live ? sb.toff[t] : 0) + slot * 4;
+      P.nd[r][j] = live ? sb.tn[t * 16 + slot] : -1;
     }
-    for (int i = 0; i < mlw[0]; i += 4) {
+}
+// one item: every node's sums over its row of the packed table, the block in LDS (HL); MODE 0: weights +-1,
+// +1: the +1 edges with weight 1, -1: the -1 edges with weight 1
+template <bool LDSW, int MODE, bool UNIT, int RB>
+__device__ __forceinline__ void sh_agg_item(const AgPairs& P, int nt16, const float4* HL, const uint16_t* tab,
+                                            int zoff, float* dst, int accumulate, int w, int lane) {
+  const int q = lane & 1;
+  typedef uint16_t __attribute__((ext_vector_type(4))) u16x4;
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const char* hb = reinterpret_cast<const char*>(HL);
+  const uint32_t qoff = 16u * (uint32_t)q;
 #pragma unroll
-      for (int j = 0; j < AG_TPW; ++j) {
-        if (i + 4 < mlw[j]) {  // wave-uniform
-          const bool ok = i + 4 < ml[j];
-          const u16x4 v = *reinterpret_cast<const u16x4*>(tab + (ok ? base[j] + (i + 4) * 16 : 0));
-          nxt[j] = ok ? v : u16x4{0, 0, 0, 0};
+  for (int r = 0; r < AG_R; ++r) {
+    if (2 * (w + r * AG_TPW * AG_NW) >= nt16) break;  // wave-uniform
+    u16x4 cur[AG_TPW], nxt[AG_TPW] = {};
+    f2v a01[AG_TPW], a23[AG_TPW];  // the lane's four sums as two packed pairs (v_pk_fma_f32)
+    // reads are never predicated: a lane past its row reads the zero words at zoff (a conditional select of the
+    // loaded value would make the compiler wait for it at once)
+#pragma unroll
+    for (int j = 0; j < AG_TPW; ++j) {
+      a01[j] = a23[j] = f2v{0.f, 0.f};
+      cur[j] = *reinterpret_cast<const u16x4*>(tab + (P.ml[r][j] > 0 ? P.base[r][j] : zoff));
+    }
+    for (int i = 0; i < P.mlw[r][0]; i += 4) {
+#pragma unroll
+      for (int j = 0; j < AG_TPW; ++j)
+        if (i + 4 < P.mlw[r][j])  // wave-uniform
+          nxt[j] = *reinterpret_cast<const u16x4*>(tab + (i + 4 < P.ml[r][j] ? P.base[r][j] + (i + 4) * 16 : zoff));
+      // this step's row reads first (RB edges of each pair at a time), then the sums
+#pragma unroll
+      for (int u0 = 0; u0 < 4; u0 += RB) {
+        float4 h[AG_TPW][RB];
+        float f[AG_TPW][RB];
+#pragma unroll
+        for (int j = 0; j < AG_TPW; ++j) {
+          if (i < P.mlw[r][j]) {  // wave-uniform
+            const uint2 wd = __builtin_bit_cast(uint2, cur[j]);
+#pragma unroll
+            for (int v = 0; v < RB; ++v) {
+              const int u = u0 + v;
+              const uint32_t w32 = (u < 2 ? wd.x : wd.y) >> (16 * (u & 1));  // high half: masked below
+              if (!UNIT) {
+                const int code = ((int)(w32 << 30)) >> 30;                    // +1, -1, 0
+                f[j][v] = (float)(MODE == 0 ? code : (MODE > 0 ? max(code, 0) : max(-code, 0)));
+              }
+              h[j][v] = *reinterpret_cast<const float4*>(hb + ((w32 & 0xFFE0u) | qoff));
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < AG_TPW; ++j) {
+          if (i < P.mlw[r][j]) {
+#pragma unroll
+            for (int v = 0; v < RB; ++v) {
+              if (UNIT) {  // every word weight 1 (padding reads the zero row): packed adds
+                a01[j] += f2v{h[j][v].x, h[j][v].y};
+                a23[j] += f2v{h[j][v].z, h[j][v].w};
+              } else {
+                a01[j] = __builtin_elementwise_fma(f2v{f[j][v], f[j][v]}, f2v{h[j][v].x, h[j][v].y}, a01[j]);
+                a23[j] = __builtin_elementwise_fma(f2v{f[j][v], f[j][v]}, f2v{h[j][v].z, h[j][v].w}, a23[j]);
+              }
+            }
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < AG_TPW; ++j) {
-        if (i < mlw[j]) {  // wave-uniform
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const uint32_t w16 = cur[j][u];
-            const float pos = (float)((w16 >> 14) & 1u), neg = (float)(w16 >> 15);
-            const float f = mode == 0 ? pos - neg : (mode > 0 ? pos : neg);
-            const float4 h = HL[(w16 & 0x7FFu) * 2 + q];
-            acc[j].x = fmaf(f, h.x, acc[j].x); acc[j].y = fmaf(f, h.y, acc[j].y);
-            acc[j].z = fmaf(f, h.z, acc[j].z); acc[j].w = fmaf(f, h.w, acc[j].w);
-          }
+        if (i < P.mlw[r][j]) {
           cur[j] = nxt[j];
         }
       }
     }
 #pragma unroll
     for (int j = 0; j < AG_TPW; ++j) {
-      if (nd[j] >= 0) {
-        float* d = dst + (size_t)nd[j] * SH_FC + 4 * q;
-        float4 o = acc[j];
+      if (P.nd[r][j] >= 0) {
+        float* d = dst + (size_t)P.nd[r][j] * SH_FC + 4 * q;
+        float4 o = make_float4(a01[j].x, a01[j].y, a23[j].x, a23[j].y);
         if (accumulate) {
           const float4 pv = f4(d);
           o = make_float4(pv.x + o.x, pv.y + o.y, pv.z + o.z, pv.w + o.w);
@@ -475,6 +533,7 @@ __device__ __forceinline__ void sh_agg_item(const SharedBufs& sb, const float4* 
 template <int XSRC>
 __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, SharedBufs sb, const float* src,
                                                                    int mode, int accumulate, int items) {
+  // mode (the host's +1 / -1 / 0 per launch) must match XSRC: 1 -> +1, 2 -> -1, 0 / 3 -> 0
   extern __shared__ __attribute__((aligned(16))) float4 HL[];  // [N][2], then the packed edge table
   const int N = a.N;
   if (mode < 0 && !(a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0)) return;  // no -1 edge: A- . V = 0
@@ -484,8 +543,23 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
   float4 pf[NPF];
   float xk0[NXT], xk1[NXT];
   int pc = 0;  // chunk of the prefetched item (XSRC)
+  // XSRC: the 8-input Linear (W0 or Wx: 64 x 8) and w_a sit at the end of the LDS (AG_WL floats), read per item
+  // (global reads inside the build would expose an L2 round trip per item; registers would spill)
+  float* WLs = reinterpret_cast<float*>(reinterpret_cast<char*>(HL) + AG_LDS) - AG_WL;
   const int wv_ = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  auto load_block = [&](int it) {
+  // the k-th item of this workgroup (-1: none).  XSRC 0: items blockIdx.x + k grid.  XSRC 1..3: the workgroup
+  // walks whole episodes, their 8 chunks in a row (episode blockIdx.x + (k / 8) grid, chunk k % 8), so an episode's
+  // x rows are loaded once for its 8 blocks (one workgroup per episode, instead of 8 reading them from the MALL)
+  auto item_of = [&](int k) -> int {
+    if (XSRC == 0) {
+      const int it = (int)blockIdx.x + k * (int)gridDim.x;
+      return it < items ? it : -1;
+    }
+    const int ep = (int)blockIdx.x + (k >> 3) * (int)gridDim.x;
+    if (ep >= items / 8) return -1;
+    return ((ep / SH_EPS) * 8 + (k & 7)) * SH_EPS + ep % SH_EPS;
+  };
+  auto load_block = [&](int it, int k) {
     if (XSRC == 0) {
       const float* S = src + (size_t)it * N * SH_FC;
 #pragma unroll
@@ -497,12 +571,20 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
       const int e = it % SH_EPS, c = (it / SH_EPS) % 8, s = it / (8 * SH_EPS);
       const int ep = s * SH_EPS + e;
       pc = c;
+      if ((k & 7) == 0)  // the episode's first chunk: its x rows (kept for the other 7)
 #pragma unroll
       for (int j = 0; j < NXT; ++j) {
-        const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
-        const bool ok = ep < a.B && n < N;
-        xk0[j] = ok ? a.x[((size_t)ep * N + n) * 8 + (ln >> 4)] : 0.f;
-        xk1[j] = ok ? a.x[((size_t)ep * N + n) * 8 + 4 + (ln >> 4)] : 0.f;
+        // unpredicated loads (a predicated load compiles to a branch and a wait per load): a padding episode
+        // reads episode B - 1's rows and reaches only its own rows; nodes past N are not stored
+        const int n = min((wv_ + j * AG_NW) * 16 + (ln & 15), N - 1);
+        const float* xr = a.x + ((size_t)min(ep, a.B - 1) * N + n) * 8 + (ln >> 4);
+#if ECO_AB_XBUILD == 2
+        xk0[j] = (float)n; xk1[j] = (float)ep;
+        (void)xr;
+#else
+        xk0[j] = xr[0];
+        xk1[j] = xr[4];
+#endif
       }
     }
   };
@@ -515,13 +597,22 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
       }
     } else {
       // lin8_chunk gives features 16 (pc / 2) + 4 (ln >> 4) ..: the lanes of 8-feature chunk pc keep theirs
-      const float4 wa = f4(a.P + PK_WA + 16 * (pc >> 1) + 4 * (ln >> 4));
       const bool mine = (ln >> 5) == (pc & 1);
+      const float* wl = WLs + (ln & 15) * 8 + (ln >> 4) + (pc >> 1) * 128;
+      const float wv0 = wl[0], wv1 = wl[4];
+      const float4 wa = XSRC == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                  : *reinterpret_cast<const float4*>(WLs + 512 + 16 * (pc >> 1) + 4 * (ln >> 4));
 #pragma unroll
       for (int j = 0; j < NXT; ++j) {
         const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
         if ((wv_ + j * AG_NW) * 16 >= N) break;  // wave-uniform: MFMAs below run with EXEC all ones
-        const f32x4 z = lin8_chunk(a.P + (XSRC == 3 ? PK_W0 : PK_WX), pc >> 1, xk0[j], xk1[j], ln);
+        // lin8_chunk on the preloaded weights (the same two MFMAs)
+#if ECO_AB_XBUILD == 1
+        f32x4 z = f32x4{xk0[j] * wv0, xk1[j] * wv1, xk0[j], xk1[j]};
+#else
+        f32x4 z = __builtin_amdgcn_mfma_f32_16x16x4f32(wv0, xk0[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_16x16x4f32(wv1, xk1[j], z, 0, 0, 0);
+#endif
         const float sg = XSRC == 2 ? -1.f : 1.f;
         float4 v = XSRC == 3 ? relu4(z)
                              : make_float4(relu(fmaf(sg, wa.x, z[0])), relu(fmaf(sg, wa.y, z[1])),
@@ -530,29 +621,45 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
       }
     }
   };
-  int item = blockIdx.x;
-  if (item >= items) return;
+  int item = item_of(0);
+  if (item < 0) return;
   const int nwords = sb.toff[sb.nt16];
-  const bool in_lds = (size_t)n2 * 16 + (size_t)nwords * 2 <= (size_t)AG_LDS;  // uniform
-  uint16_t* T16 = reinterpret_cast<uint16_t*>(HL + n2);                         // 16-B aligned
+  // LDS: the block's N rows, the zero row N, the packed table ... the x-build weights at the end
+  const bool in_lds = (size_t)(n2 + 2) * 16 + (size_t)(nwords + AG_ZW) * 2 + AG_WL * 4 <= (size_t)AG_LDS;  // uniform
+  if (XSRC)
+    for (int i = threadIdx.x; i < AG_WL; i += 64 * AG_NW)
+      WLs[i] = i < 512 ? a.P[(XSRC == 3 ? PK_W0 : PK_WX) + i] : (i < 576 ? a.P[PK_WA + i - 512] : 0.f);
+  uint16_t* T16 = reinterpret_cast<uint16_t*>(HL + n2 + 2);                           // 16-B aligned
+  // no -1 edge and N < 2048 (padding on the zero row): every word is a +1 edge (A+ = A; the A- pass returned above)
+  const bool unit = N < 2048 && !(a.gs.meta[(size_t)a.gids[0] * 4 + 2] < 0.0);
+  if (threadIdx.x < 2) HL[n2 + threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (in_lds) {
     const uint4* s4p = reinterpret_cast<const uint4*>(sb.et16);
     uint4* d4p = reinterpret_cast<uint4*>(T16);
-    for (int i = threadIdx.x; i < nwords / 8; i += 64 * AG_NW) d4p[i] = s4p[i];  // nwords: a multiple of 64
+    for (int i = threadIdx.x; i < (nwords + AG_ZW) / 8; i += 64 * AG_NW) d4p[i] = s4p[i];  // multiples of 64
   }
-  load_block(item);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  AgPairs P;
+  sh_agg_pairs(sb, P, w, lane);
+  if (XSRC) __syncthreads();  // the x-build weights
+  load_block(item, 0);
   store_block();
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (; item < items; item += gridDim.x) {
-    const bool more = item + (int)gridDim.x < items;
-    if (more) load_block(item + gridDim.x);  // lands while this item is aggregated
+  constexpr int MODE = XSRC == 1 ? 1 : (XSRC == 2 ? -1 : 0);  // U over +1 edges, V over -1 edges, else signed
+  for (int k = 0; item >= 0; ++k) {
+    const int next = item_of(k + 1);
+    const bool more = next >= 0;
+    if (more) load_block(next, k + 1);  // lands while this item is aggregated
     float* dst = sb.AG + (size_t)item * N * SH_FC;
-    if (in_lds) sh_agg_item<true>(sb, HL, T16, dst, N, mode, accumulate, w, lane);
-    else sh_agg_item<false>(sb, HL, sb.et16, dst, N, mode, accumulate, w, lane);
+    // row reads in flight per pair: 4 edges (2: measured slower where the x prefetch holds registers)
+    constexpr int RB = 4;
+    if (in_lds && unit) sh_agg_item<true, MODE, true, RB>(P, sb.nt16, HL, T16, nwords, dst, accumulate, w, lane);
+    else if (in_lds) sh_agg_item<true, MODE, false, RB>(P, sb.nt16, HL, T16, nwords, dst, accumulate, w, lane);
+    else sh_agg_item<false, MODE, false, RB>(P, sb.nt16, HL, sb.et16, nwords, dst, accumulate, w, lane);
     __syncthreads();  // every wave is done with this block
     if (more) store_block();
     __syncthreads();
+    item = next;
   }
 }
 
@@ -607,9 +714,10 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
 #pragma unroll
         for (int c = 0; c < 4; ++c) R.hc[c] = f4_nt(Hc + ro + c * cs);
       } else {
-        const bool ok = ep < a.B && n < N;
-        R.xk0 = ok ? a.x[((size_t)ep * N + n) * 8 + s4] : 0.f;
-        R.xk1 = ok ? a.x[((size_t)ep * N + n) * 8 + 4 + s4] : 0.f;
+        // unpredicated (clamped) loads: rows of padding episodes and nodes are stored as zeros
+        const float* xr = a.x + ((size_t)min(ep, a.B - 1) * N + nc) * 8 + s4;
+        R.xk0 = xr[0];
+        R.xk1 = xr[4];
       }
     }
   };
