@@ -186,8 +186,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "final", "train_pmc_hbm.json")
-PMC_SQ = os.path.join(REPO, "profiles", "r03", "final", "pmc_sq_dense.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r04", "final", "train", "pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r04", "final", "train", "pmc_sq_dense.json")
 PMC_PAIRED = True  # the committed train PMC pass ran the paired s' forward (eco_mpnn_forward_pair)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
 
@@ -219,7 +219,7 @@ WGRAD_NAMES = ("wgrad_fh_kernel", "wgrad_bf3_kernel", "wgrad_kernel")
 
 def _first(d, names):
     return next(d[k] for k in names if k in d)
-PMC_GSET = os.path.join(REPO, "profiles", "r02", "gset_pmc", "pmc_hbm.json")
+PMC_GSET = os.path.join(REPO, "profiles", "r04", "final", "gset_pmc", "pmc_hbm.json")
 
 
 def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
