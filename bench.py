@@ -47,14 +47,25 @@ def envstep_alg_bytes(n):
     return n + 14.25 * n + 28.0 * n
 
 
-def envstep_roofline(rate, ms, n):
-    """env_step_roofline object from a measured env-step rate (env-steps/s) and mean launch time."""
+def envstep_roofline(rate, ms, n, B=None):
+    """env_step_roofline object from a measured env-step rate (env-steps/s) and mean launch time; traffic = the
+    PMC HBM bytes per launch of the committed train profile (ER-200 x 8192 only)."""
     bpe = envstep_alg_bytes(n)
     achieved = bpe * rate / 1e9
-    return {"bound": "hbm", "kernel": "env_step_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "alg_bytes_per_env_step": bpe, "env_steps_per_s": rate,
-            "avg_launch_ms": ms, "source": "SURVEY.md 8d incremental bytes x the env step kernel's rate "
-                                          "(HIP events, random actions, same B and N)"}
+    traffic = None
+    if n == 200 and B == 8192:
+        try:
+            with open(PMC_SUMMARY) as f:
+                k = json.load(f)["kernels"]
+            traffic = k["env_step_fast_kernel"][str(B // 4)]["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
+    return {"bound": "hbm", "kernel": "env_step_fast_kernel" if n <= 256 else "env_step_kernel",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC, %s)" % os.path.relpath(PMC_SUMMARY, REPO),
+            "alg_bytes_per_launch": bpe * B if B else None, "alg_bytes_per_env_step": bpe, "env_steps_per_s": rate,
+            "avg_launch_ms": ms, "source": "SURVEY.md 8d incremental bytes x the env step kernel's rate (launches "
+                                          "replayed from a HIP graph, HIP events, random actions, same B and N)"}
 
 
 def mpnn_flops(nnz, n):
@@ -287,7 +298,7 @@ def pmc_traffic(dom, B, M, n, graph="ER"):
 def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234, store=None):
     """The batched MaxCut env step kernel alone (spinsystem.py:355-559, ER(n, 0.15) +-1 graphs -- or the
     given store's graphs -- one per episode, uniform random actions drawn beforehand): env-steps/s over
-    `steps` launches timed with HIP events on the launch stream, and the mean launch time (ms)."""
+    `steps` launches replayed from a HIP graph and timed with HIP events, and the mean launch time (ms)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget
@@ -304,10 +315,20 @@ def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234, store=None):
     for i in range(warmup):
         env.step(acts[i])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the launches are replayed from a HIP graph: a Python loop of ctypes launches (~20-30 us of host time each)
+    # cannot keep a ~20 us kernel busy, and the events would time the host.  Graph replay issues them back to back
+    # (one kernel boundary each, ~1.5 us), which is what the kernel's rate is.
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(device=dev)
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):
+        with torch.cuda.graph(graph, stream=cap):
+            for i in range(steps):
+                env.step(acts[warmup + i])
+    torch.cuda.current_stream(dev).wait_stream(cap)
     torch.cuda.synchronize()
     e0.record()
-    for i in range(steps):
-        env.step(acts[warmup + i])
+    graph.replay()
     e1.record()
     torch.cuda.synchronize()
     env.check_errors()
@@ -641,7 +662,7 @@ def main():
         }
         # the env step kernel alone on this bench's graphs: SURVEY.md 8d's HBM roofline of the env step
         es_rate, es_ms = envstep_rate(dev, B, n, store=store)
-        out["env_step_roofline"] = envstep_roofline(es_rate, es_ms, n)
+        out["env_step_roofline"] = envstep_roofline(es_rate, es_ms, n, B)
         out["untimed_per_episode_costs"] = fixed
         mf = pmc_mfma(dom, B, args.minibatch, n, args.graph, mean_gf) if train else None
         if mf:
@@ -794,15 +815,24 @@ def envstep_bench(args, world, rank, local, dev, dist):
     for i in range(args.warmup):
         env.step(acts[i])
     env.check_errors()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # the K launches are captured once in a HIP graph and replayed (a Python loop of ctypes launches costs ~20-30
+    # us of host time per launch, more than the kernel: timed that way, the host is measured)
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(device=dev)
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):
+        with torch.cuda.graph(graph, stream=cap):
+            for i in range(steps):
+                env.step(acts[args.warmup + i])
+    torch.cuda.current_stream(dev).wait_stream(cap)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        evs[i][0].record()
-        env.step(acts[args.warmup + i])
-        evs[i][1].record()
+    e0.record()
+    graph.replay()
+    e1.record()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -811,7 +841,7 @@ def envstep_bench(args, world, rank, local, dev, dist):
     dt = max_over_ranks(dt_rank, device=dev)
     pg = process_group_info(world, dt_rank, steps, local, dev)
     env.check_errors()
-    k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    k_ms = e0.elapsed_time(e1) / steps
     nnz = float(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
     W = _lib.obs_x_stride(len(obs))
     per_step = B * (n * (2 * (1 + 4 + 2) + 1 + 4 * W) + 4 * nnz / n + 2 * 192 +
