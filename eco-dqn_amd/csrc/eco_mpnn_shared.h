@@ -46,12 +46,8 @@ namespace eco {
 constexpr int SH_EPS = 4;              // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per Linear tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
 constexpr int SH_NW = SH_NW_X;         // waves per Linear workgroup (one workgroup per CU: <= 128 VGPRs at 16)
-#ifndef SH_PREFETCH
-#define SH_PREFETCH 0                  // 1: the next tile's rows are loaded while the current tile computes (measured
-                                       // slower: 3.96 ms per configs[4] step with 16 waves (49 VGPRs spill), 3.69
-                                       // with 8, against 3.56 without)
-#endif
-constexpr int SH_PART = SH_EPS * 64;   // floats of one tile's column-sum partial
+constexpr int SH_PART = SH_EPS * 64;   // floats of one column-sum partial
+constexpr int SH_RUN = 8;              // consecutive tiles per wave item of the last Linear launch (one partial)
 #ifndef AG_NW_X
 #define AG_NW_X 16
 #endif
@@ -67,7 +63,8 @@ struct SharedBufs {
   float* HB;      //  first update layer rebuild them from the observation rows, 32 B per node instead of 256 B)
   float* EB;
   float* AG;      // the aggregation of the current phase (raw neighbour sums, not yet divided by the degree)
-  float* part;    // [S][ntiles][SH_EPS][64] column-sum partials of h3, one per Linear tile
+  float* part;    // [2 x groups][SH_EPS][64] column-sum partials of h3: one per (group of SH_RUN consecutive Linear
+                  // tiles, slice the group touches)
   float* ql;      // [Epad][N] Wr[64:] . h3
   int32_t* perm;  // [N] nodes by decreasing degree
   int32_t* tn;    // [nt16][16] aggregation tiles: node of each slot (-1: none), 16 ranked nodes per tile
@@ -91,11 +88,14 @@ inline int shared_grid() {  // persistent Linear workgroups: one per CU
   return g;
 }
 
+inline size_t shared_part_slots(int N, int B) {  // two per group of SH_RUN tiles (a group spans <= 2 slices)
+  const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
+  return 2 * ((S * nt + SH_RUN - 1) / SH_RUN);
+}
 inline size_t shared_ws_bytes(int N, int B) {
   const size_t S = ((size_t)B + SH_EPS - 1) / SH_EPS, Epad = S * SH_EPS;
-  const size_t nt = ((size_t)N + SH_NPT - 1) / SH_NPT;
   const size_t nt16 = ((size_t)N + 15) / 16, MD = ((size_t)N + 3) / 4 * 4 + AG_UNROLL;
-  return (4 * (size_t)N * Epad * 64 + S * nt * SH_PART + Epad * (size_t)N + N + nt16 * 17 + 4 + nt16 * MD * 16 +
+  return (4 * (size_t)N * Epad * 64 + shared_part_slots(N, B) * SH_PART + Epad * (size_t)N + N + nt16 * 17 + 4 + nt16 * MD * 16 +
           nt16 * MD * 8 + nt16 + 1 + 4) *
          sizeof(float);
 }
@@ -112,7 +112,8 @@ inline SharedBufs shared_carve(float* base, int N, int B) {
   sb.EB = sb.HB + T1;
   sb.AG = sb.EB + T1;
   sb.part = sb.AG + T1;
-  sb.ql = sb.part + (size_t)sb.S * sb.ntiles * SH_PART;
+  sb.ql = sb.part + shared_part_slots(N, B) * SH_PART;
+
   sb.perm = reinterpret_cast<int32_t*>(sb.ql + (size_t)sb.Epad * N);
   sb.nt16 = (N + 15) / 16;
   sb.MD = (N + 3) / 4 * 4 + AG_UNROLL;
@@ -721,19 +722,18 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       }
     }
   };
-  int item = blockIdx.x * SH_NW + w;
-#if SH_PREFETCH
-  Rows nx;
-  if (item < total) load_rows(nx, item);
-#endif
-  for (; item < total; item += gridDim.x * SH_NW) {
-#if SH_PREFETCH
-    const Rows cu = nx;
-    if (item + gridDim.x * SH_NW < total) load_rows(nx, item + gridDim.x * SH_NW);
-#else
+  // items strided over the waves; the last layer (PHASE 2) strides groups of SH_RUN consecutive tiles, so each
+  // wave's column sums accumulate over a group in registers and leave as one partial per (group, slice it touches)
+  const int wid = blockIdx.x * SH_NW + w;
+  const int waves = gridDim.x * SH_NW;
+  constexpr int RUN = PHASE == 2 ? SH_RUN : 1;
+  float4 run[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) run[nt] = zero4();
+  for (int it = wid * RUN; it < total; it += waves * RUN)
+  for (int item = it; item < min(total, it + RUN); ++item) {
     Rows cu;
     load_rows(cu, item);
-#endif
     const int s = item / sb.ntiles, t = item - s * sb.ntiles;
     const int ep = s * SH_EPS + eps;
     const bool evalid = ep < a.B;
@@ -816,7 +816,9 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
         }
       } else {
         float qp = 0.f;
-        float* pt = sb.part + ((size_t)s * sb.ntiles + t) * SH_PART + eps * 64 + 4 * s4;
+        const bool flush = item + 1 >= min(total, it + RUN) || (item + 1) / sb.ntiles != s;  // wave-uniform
+        const int slot = 2 * (it / RUN) + (s - it / sb.ntiles);
+        float* pt = sb.part + (size_t)slot * SH_PART + eps * 64 + 4 * s4;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const float4 h3 = rvalid ? relu4(hn[nt]) : zero4();
@@ -825,14 +827,18 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
           qp = fmaf(h3.y, P[PK_WR + 65 + f], qp);
           qp = fmaf(h3.z, P[PK_WR + 66 + f], qp);
           qp = fmaf(h3.w, P[PK_WR + 67 + f], qp);
-          // the tile's column sums over its SH_NPT nodes (fixed butterfly order), one partial per tile
+          // the tile's column sums over its SH_NPT nodes (fixed butterfly order), added to the run's in tile order
           float4 csum = h3;
 #pragma unroll
           for (int o = SH_EPS; o < 16; o <<= 1) {
             csum.x += __shfl_xor(csum.x, o, 64); csum.y += __shfl_xor(csum.y, o, 64);
             csum.z += __shfl_xor(csum.z, o, 64); csum.w += __shfl_xor(csum.w, o, 64);
           }
-          if (kn == 0) st4_nt(pt + 16 * nt, csum);
+          run[nt] = make_float4(run[nt].x + csum.x, run[nt].y + csum.y, run[nt].z + csum.z, run[nt].w + csum.w);
+          if (flush) {
+            if (kn == 0) st4_nt(pt + 16 * nt, run[nt]);
+            run[nt] = zero4();
+          }
         }
         qp += __shfl_xor(qp, 16, 64);
         qp += __shfl_xor(qp, 32, 64);
@@ -851,11 +857,15 @@ __global__ __launch_bounds__(256) void shared_readout_kernel(MpnnArgs a, SharedB
   const int N = a.N;
   const float* P = a.P;
   const int s = e / SH_EPS, er = e % SH_EPS;
-  {  // the slice's per-tile column sums: wave w takes tiles w, w + 4, ...; the four combined in order
-    const float* pp = sb.part + (size_t)s * sb.ntiles * SH_PART + er * 64 + lane;
+  {  // the slice's column sums: the partials of the tile groups touching slice s (group g = tiles [g SH_RUN,
+     // (g + 1) SH_RUN) of the slice-major order, partial 2 g + (s - first slice of g)); wave w of this block takes
+     // groups g0 + w, + 4, ..., the four combined in order
+    const int g0 = s * sb.ntiles / SH_RUN, g1 = ((s + 1) * sb.ntiles - 1) / SH_RUN;
     float c0 = 0.f;
-#pragma unroll 8
-    for (int k = w; k < sb.ntiles; k += 4) c0 += pp[(size_t)k * SH_PART];
+    for (int g = g0 + w; g <= g1; g += 4) {
+      const int slot = 2 * g + (s - g * SH_RUN / sb.ntiles);
+      c0 += sb.part[(size_t)slot * SH_PART + er * 64 + lane];
+    }
     red[w][lane] = c0;
   }
   __syncthreads();
