@@ -257,16 +257,20 @@ __device__ __forceinline__ AggScale agg_scale(const int* TE, int ntiles, int lan
 
 // B fragment (8 fp16 adjacency entries of the lane's node for the chunk's k slots) from a spread word; PPlo / PPhi:
 // magnitude patterns of the chunk's two tiles.  MODE 0: A (signed); 1: A+ = [A = +1]; 2: A- = [A = -1] as +1.
+// Per dword t: the 0/1 edge bits of the two halves times the magnitude pattern in one v_pk_mul_lo_u16, and (MODE 0)
+// the sign bits moved to bits 15 / 31 in one v_and_or: 5 VALU per dword instead of 7 (the adjacency fragments are
+// the largest VALU item of the aggregations; bitwise the same fragments)
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 template <int MODE>
 __device__ __forceinline__ f16x8 adj_frag2(uint32_t W, uint32_t PPlo, uint32_t PPhi) {
+  const uint32_t Wm = MODE == 0 ? W : (MODE == 1 ? (W & ~(W >> 4)) : (W >> 4));  // bit t: edge (+1 edge, -1 edge)
   u32x4v d;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const uint32_t PP = t < 2 ? PPlo : PPhi;
-    const uint32_t nz = (W >> t) & 0x10001u, ng = (W >> (t + 4)) & 0x10001u;
-    const uint32_t on = MODE == 0 ? nz : (MODE == 1 ? (nz & ~ng) : ng);
-    uint32_t v = (on * 0xFFFFu) & PP;
-    if (MODE == 0) v |= ng << 15;
+    const u16x2v on = __builtin_bit_cast(u16x2v, (Wm >> t) & 0x10001u);
+    uint32_t v = __builtin_bit_cast(uint32_t, on * __builtin_bit_cast(u16x2v, PP));
+    if (MODE == 0) v |= (W << (11 - t)) & 0x80008000u;  // -1 edge bits t + 4, t + 20 -> signs 15, 31
     d[t] = v;
   }
   return __builtin_bit_cast(f16x8, d);
