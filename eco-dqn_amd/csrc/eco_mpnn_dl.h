@@ -138,9 +138,8 @@ __device__ __forceinline__ void dl_agg(f32x4 (&acc)[DL_MT][2], const uint16_t* P
 #pragma unroll
         for (int i = 0; i < DL_MT; ++i) {
           if (i >= ntw) break;  // wave-uniform
-          const uint32_t wd = adj[i][0];
-          const uint32_t pre = h ? (wd >> 16) : (wd & 0xFFFFu);
-          const uint32_t W = (pre & 0xFFu) | ((pre & 0xFF00u) << 8);
+          // the chunk's 16-bit word, its bytes spread to bits 0-7 and 16-23 (one v_perm_b32)
+          const uint32_t W = __builtin_amdgcn_perm(0u, adj[i][m], h ? 0x0C030C02u : 0x0C010C00u);
           const f16x8 bf = adj_frag2<MODE>(W, plo, phi);
 #pragma unroll
           for (int p = 1; p >= 0; --p)  // the small plane first
@@ -150,13 +149,6 @@ __device__ __forceinline__ void dl_agg(f32x4 (&acc)[DL_MT][2], const uint16_t* P
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // bound the fragments in flight to the next chunk's
-    }
-#pragma unroll
-    for (int i = 0; i < DL_MT; ++i) {
-      const uint32_t w0 = adj[i][0];
-#pragma unroll
-      for (int k = 0; k + 1 < DL_AW; ++k) adj[i][k] = adj[i][k + 1];
-      adj[i][DL_AW - 1] = w0;
     }
   }
 }
