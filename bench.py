@@ -761,7 +761,8 @@ def inference_bench(args, world, rank, local, dev, dist):
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": ("f32-accurate MPNN on f16 MFMA (fp16x2 splits)" if n <= 512 else
-                      "f32-accurate MPNN on bf16 MFMA (bf16x3 splits)") + " / f64+int (env)",
+                      "f32-accurate MPNN: Linears on f16 MFMA (fp16x2 splits), aggregations in f32 from LDS") +
+                     " / f64+int (env)",
             "data": "synthetic: seeded graphs; random-init MPNN (std 0.1)",
             "config": {"workload": f"{name} x{B} episodes/GPU: MPNN fwd + greedy act + env step "
                                    f"({'configs[4]' if args.workload == 'gset' else 'configs[1]'})",
