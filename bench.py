@@ -18,7 +18,7 @@ Prints ONE JSON line on rank 0 with
   roofline: dominant kernel measured live with HIP events (on the launch stream),
             algorithmic FLOPs from SURVEY.md 8d: forward F = 1392*nnz + 107,648*N + 8,192
             per graph, backward = 2F; peak = the dense peak of the MFMA dtype the kernel ISSUES
-            (f16 / bf16, 2.5 PFLOP/s: the fp16x2 / bf16x3 split kernels), frac <= 1 by construction;
+            (f16 / bf16, 2.5 PFLOP/s: the fp16x2 split kernels; bf16x3 in the per-episode N > 512 one), frac <= 1 by construction;
             the f32-MFMA figure (157.3) is kept as a separately named field.
   env_step_roofline: the env step kernel alone (same B, N), SURVEY.md 8d incremental algorithmic bytes
             per env-step (N + 14.25 N + 28 N) x rate / HBM peak (8 TB/s).
@@ -206,7 +206,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak
 def forward_kernel_name(n, graph, n_graphs=None):
     """The forward kernel the dispatcher runs for 8-feature rows and +-1 / unit weights (eco_mpnn_forward):
     blocks of <= 224 rows -> the fp16x2 dense kernels; one graph of 224 < N <= 512 -> the fp16x2 DL kernels;
-    N > 512 on one shared graph -> the shared-graph kernels (bf16x3 Linears).  All issue f16/bf16 MFMAs."""
+    N > 512 on one shared graph -> the shared-graph kernels (fp16x2 Linears).  All issue f16/bf16 MFMAs."""
     if n <= 224:
         return "mpnn_forward_dense2_kernel"
     if n <= 512:
@@ -216,8 +216,8 @@ def forward_kernel_name(n, graph, n_graphs=None):
 
 def mfma_roofline(achieved_tflops, kernel):
     """roofline fields for an MPNN kernel: frac against the dense peak of the MFMA dtype it issues (f16 for
-    the fp16x2 dense / DL kernels, bf16 for the bf16x3 shared-graph Linears, both 2.5 PF; f32 157.3 TF for the
-    per-episode large kernel's f32 MFMAs is not used there either: it also runs bf16x3 fragments)."""
+    the fp16x2 dense / DL kernels and the shared-graph Linears, 2.5 PF; f32 157.3 TF is not used for the
+    per-episode large kernel either: it runs bf16x3 fragments, the bf16 peak being the same 2.5 PF)."""
     peak = F16_MFMA_PEAK_TFLOPS
     return {"bound": "mfma", "kernel": kernel, "achieved": achieved_tflops, "peak": peak, "unit": "TFLOP/s",
             "frac": achieved_tflops / peak, "peak_dtype": "f16/bf16 dense MFMA (the issued dtype)",
