@@ -37,9 +37,6 @@ namespace eco {
 #ifndef SH_NW_X
 #define SH_NW_X 16
 #endif
-#ifndef ECO_AB_XBUILD
-#define ECO_AB_XBUILD 0                // A/B timing probes only (wrong results): 1 no MFMA in the x build, 2 no x loads
-#endif
 #ifndef ECO_AB_SHARED_BF3
 #define ECO_AB_SHARED_BF3 0            // A/B builds only (tools/): the round-3 six-product bf16x3 Linears
 #endif
@@ -579,13 +576,8 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
         // reads episode B - 1's rows and reaches only its own rows; nodes past N are not stored
         const int n = min((wv_ + j * AG_NW) * 16 + (ln & 15), N - 1);
         const float* xr = a.x + ((size_t)min(ep, a.B - 1) * N + n) * 8 + (ln >> 4);
-#if ECO_AB_XBUILD == 2
-        xk0[j] = (float)n; xk1[j] = (float)ep;
-        (void)xr;
-#else
         xk0[j] = xr[0];
         xk1[j] = xr[4];
-#endif
       }
     }
   };
@@ -608,12 +600,8 @@ __global__ __launch_bounds__(64 * AG_NW, 1) void shared_agg_kernel(MpnnArgs a, S
         const int n = (wv_ + j * AG_NW) * 16 + (ln & 15);
         if ((wv_ + j * AG_NW) * 16 >= N) break;  // wave-uniform: MFMAs below run with EXEC all ones
         // lin8_chunk on the preloaded weights (the same two MFMAs)
-#if ECO_AB_XBUILD == 1
-        f32x4 z = f32x4{xk0[j] * wv0, xk1[j] * wv1, xk0[j], xk1[j]};
-#else
         f32x4 z = __builtin_amdgcn_mfma_f32_16x16x4f32(wv0, xk0[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         z = __builtin_amdgcn_mfma_f32_16x16x4f32(wv1, xk1[j], z, 0, 0, 0);
-#endif
         const float sg = XSRC == 2 ? -1.f : 1.f;
         float4 v = XSRC == 3 ? relu4(z)
                              : make_float4(relu(fmaf(sg, wa.x, z[0])), relu(fmaf(sg, wa.y, z[1])),
