@@ -13,9 +13,9 @@
 //   * Aggregation agg[f][i] = sum_j H[j][f] A[j][i]: the planes hold H of tile t (16 rows) scaled by 2^k_t (k_t
 //     from the tile's max |h|, written by the wave that owns the tile next to its planes); the adjacency operand,
 //     built in registers from bitmasks, carries +-2^(c - k_t) instead of +-1 (exact in fp16 for
-//     c - k_t in [-24, 15]; c = 15 + min_t k_t per aggregation), so every product is h 2^c and the f32 sum is
-//     scaled back by 2^-c -- folded into the 1/norm multiply.  Rows of a tile more than 2^39 below the block's
-//     largest tile get a zero operand (they contribute < 2^-39 of the largest term).
+//     c - k_t in [-21, 15]; c = 15 + min_t k_t per aggregation), so every product is h 2^c and the f32 sum is
+//     scaled back by 2^-c -- folded into the 1/norm multiply.  Rows of a tile more than 2^36 below the block's
+//     largest tile get a zero operand (they contribute < 2^-36 of the largest term).
 //   * Linears: weights pre-split per matrix (PK_FH, scale 2^kw); activations scaled per node by 2^kx (node max
 //     over the Linear's 64 or 128 inputs: four lanes hold one node, combined with permlane swaps), unscaled by
 //     2^-(kx + kw) after the f32 accumulation.
@@ -250,7 +250,7 @@ __device__ __forceinline__ AggScale agg_scale(const int* TE, int ntiles, int lan
   s.c = kmin == D2_K_EMPTY ? 0 : 15 + kmin;
   const int E = s.c - k;  // <= 15 by the choice of c
   uint32_t p = 0u;
-  if (k != D2_K_EMPTY) p = E >= -14 ? (uint32_t)(E + 15) << 10 : (E >= -24 ? 1u << (E + 24) : 0u);
+  if (k != D2_K_EMPTY) p = E >= -14 ? (uint32_t)(E + 15) << 10 : (E >= -21 ? 1u << (E + 24) : 0u);
   s.pat = p | (p << 16);
   return s;
 }
@@ -267,8 +267,10 @@ __device__ __forceinline__ f16x8 adj_frag2(uint32_t W, uint32_t PPlo, uint32_t P
   u32x4v d;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const uint32_t PP = t < 2 ? PPlo : PPhi;
-    const u16x2v on = __builtin_bit_cast(u16x2v, (Wm >> t) & 0x10001u);
+    // the edge bit stays at bit t (value 2^t) and the pattern is shifted down instead (scalar, uniform): exact, the
+    // patterns having no bit below bit 3 (agg_scale: normal fp16 powers of two, subnormals down to 2^-21 only)
+    const uint32_t PP = (t < 2 ? PPlo : PPhi) >> t;
+    const u16x2v on = __builtin_bit_cast(u16x2v, Wm & (0x10001u << t));
     uint32_t v = __builtin_bit_cast(uint32_t, on * __builtin_bit_cast(u16x2v, PP));
     if (MODE == 0) v |= (W << (11 - t)) & 0x80008000u;  // -1 edge bits t + 4, t + 20 -> signs 15, 31
     d[t] = v;

@@ -94,7 +94,7 @@ __device__ __forceinline__ AggScale dl_agg_scale(const int* TE, int ntiles, int 
   s.c = kmin == D2_K_EMPTY ? 0 : 15 + kmin;
   const int E = s.c - k;
   uint32_t p = 0u;
-  if (k != D2_K_EMPTY) p = E >= -14 ? (uint32_t)(E + 15) << 10 : (E >= -24 ? 1u << (E + 24) : 0u);
+  if (k != D2_K_EMPTY) p = E >= -14 ? (uint32_t)(E + 15) << 10 : (E >= -21 ? 1u << (E + 24) : 0u);
   s.pat = p | (p << 16);
   return s;
 }
