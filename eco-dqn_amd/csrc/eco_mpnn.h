@@ -147,13 +147,9 @@ inline int device_cu_count() {
   }();
   return cus;
 }
-#ifndef ECO_AB_GPB
-#define ECO_AB_GPB 0  // A/B builds only (tools/): force this many graphs per block
-#endif
 inline int graphs_per_block(int N, int B) {
   const int cus = device_cu_count();
   const int gmax = N >= 208 ? 1 : 208 / N;
-  if (ECO_AB_GPB > 0) return ECO_AB_GPB < gmax ? ECO_AB_GPB : gmax;
   int best = gmax;
   double best_cost = 1e300;
   for (int g = gmax; g >= 1 && 2 * g >= gmax; --g) {

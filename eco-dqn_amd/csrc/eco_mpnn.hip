@@ -1112,9 +1112,6 @@ extern "C" size_t eco_mpnn_saved_bytes(int32_t n_spins, int32_t batch) {
   return sv_mask_offset_floats(RT, batch) * sizeof(float) + RT * 4 * SM_TENSORS * sizeof(uint16_t);
 }
 
-#ifndef ECO_AB_NW
-#define ECO_AB_NW 0  // A/B builds only (tools/): force the CSR kernels' wave count
-#endif
 static std::atomic<int> g_kernel_paths{0};
 int eco::kernel_paths() { return g_kernel_paths.load(std::memory_order_relaxed); }
 
@@ -1148,7 +1145,7 @@ static KCfg pick_cfg(int N, int gpb, bool backward) {
   const int rows_pad = (gpb * N + 15) & ~15;
   const int ntiles = rows_pad / 16;
   KCfg c;
-  constexpr int force_nw = ECO_AB_NW;
+  constexpr int force_nw = 0;  // (A/B builds of round 2 forced the wave count here)
   for (int nw : {16, 8, 4}) {
     if (force_nw && nw != force_nw && nw != 4) continue;
     if (backward && nw == 16) continue;  // the backward's 8-wide weight fragments need > 128 VGPRs
@@ -1244,11 +1241,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   }
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
-#if ECO_AB_DENSE_V1
-    return mpnn_forward_dense_launch(a, saved != nullptr, st);
-#else
     return mpnn_forward_dense2_launch(a, saved != nullptr, st);
-#endif
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_forward_dl_launch(a, saved != nullptr, workspace, st);
@@ -1309,11 +1302,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.gr = (float*)gradws;
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
-#if ECO_AB_DENSE_V1
-    return mpnn_backward_dense_launch(a, st);
-#else
     return mpnn_backward_dense2_launch(a, st);
-#endif
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_backward_dl_launch(a, st);

@@ -439,625 +439,5 @@ __device__ __forceinline__ void lin8(f32x4 (&d)[4], const float* W, float xk0, f
   }
 }
 
-#if ECO_AB_DENSE_V1
-// The round-2 bf16x3 kernels, superseded by eco_mpnn_dense2.h (fp16x2).  Compiled only into A/B builds
-// (-DECO_AB_DENSE_V1=1, tools/); the product library has no path to them.
-// LDS: PL 3 bf16 planes [4][DN_KPMAX][16] (also the adjacency bits while they are built, and fp32
-//      [rows][LDH] h3 rows for the readout) | WP a staged Linear (48 fragments; readout scratch) |
-//      WX the prefetched h-half of the update Linear (24 fragments) | RI [rows_pad] int2 | GB [gpb] i64 | MD [gpb]
-template <bool SAVE>
-__global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_forward_dense_kernel(MpnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  ECO_TS(0);
-  constexpr int NW = DN_NW;
-  constexpr int NT = 64 * NW;
-  const int lane = threadIdx.x & 63;
-  const int w = uniform_i(threadIdx.x >> 6);
-  const int blk = blockIdx.x;
-  const int N = a.N;
-  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
-  const int rows_valid = g_valid * N;
-  const int rows_pad = (a.gpb * N + 15) & ~15;
-  const int ntiles = rows_pad >> 4;
-  const int KP = (rows_pad + 31) & ~31;  // plane rows touched by any k-chunk
-  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
-  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);  // [rows_pad][DN_ADJW] while the bitmask is built
-  uint16_t* WP = PL + 3 * DN_PLANE;
-  uint16_t* WX = WP + 2 * BF_HALF;
-  int2* RI = reinterpret_cast<int2*>(WX + BF_HALF);
-  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
-  int* MD = reinterpret_cast<int*>(GB + a.gpb);
-  const size_t R0 = (size_t)blk * a.gpb * N;
-  const size_t RT = (size_t)a.B * N;
-  const float* P = a.P;
-  const uint16_t* PB = reinterpret_cast<const uint16_t*>(P + PK_BF);
-  const int s4 = lane >> 4;
-  const int c16 = lane & 15;
-
-  // this lane's node (tile w, row w * 16 + c16) and its features k = s4, 4 + s4: the B operand of the
-  // 8-input Linears (lin8), loaded before the staging so their latency overlaps it
-  const bool has_tile = w < ntiles;
-  const int r = w * 16 + c16;
-  const bool valid = has_tile && r < rows_valid;
-  float xk0 = 0.f, xk1 = 0.f;
-  if (valid) {
-    xk0 = a.x[(R0 + r) * 8 + s4];
-    xk1 = a.x[(R0 + r) * 8 + 4 + s4];
-  }
-  // ---- staging: Wf fragments (LDS-DMA), row info, per-graph edge base / max degree, zeroed pad rows ----
-  glds_frags<NW>(WP, PB + BF_WF, 24, w, lane);
-  for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
-  for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
-    const int gid = a.gids[blk * a.gpb + gl];
-    GB[gl] = a.gs.edge_base[gid];
-    MD[gl] = a.gs.max_deg[gid];
-  }
-  __syncthreads();
-  ECO_TS(1);
-  // this lane's k-chunk range; its adjacency bits in registers
-  const int rr = min(r, rows_pad - 1);
-  const RowInfo ri = row_info(RI, rr);
-  const float nf = (float)ri.norm;
-  const int g_lo = min(w * 16, rows_pad - 1) / N, g_hi = min(w * 16 + 15, rows_pad - 1) / N;
-  const int kc0 = (g_lo * N) >> 5;
-  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
-  uint32_t adjb[4];
-  dense_adjacency<NT>(a, ADJ, RI, GB, blk, rows_pad, rows_valid, r, rr, valid, s4, adjb);
-  // plane rows [rows_pad, KP) are read (as zeros) by the last k-chunk; no tile writes them
-  for (int i = threadIdx.x; i < (KP - rows_pad) * 3 * 4 * 4; i += NT) {
-    const int k = i & 3, ft = (i >> 2) & 3, p = (i >> 4) % 3, j = rows_pad + (i >> 4) / 3;
-    *reinterpret_cast<uint2*>(PL + p * DN_PLANE + plane_off(ft, j, k)) = make_uint2(0u, 0u);
-  }
-  auto wa_of = [&](int c) { return f4(P + PK_WA + 16 * c + 4 * s4); };  // w_a of features 16c + 4 s4 .. +3
-
-  // ---- phase A: Z = Wx . x (f32 MFMA per tile); U = relu(Z + w_a) planes ----
-  if (has_tile) {
-    f32x4 z[4];
-    lin8(z, P + PK_WX, xk0, xk1, lane);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float4 wa = wa_of(c);
-      plane_store4(PL, c, r, s4, valid ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
-                                                     relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
-                                       : zero4());
-    }
-  }
-  glds_wait();  // Wf fragments
-  __syncthreads();
-  ECO_TS(2);
-
-  // ---- phase B: edge embedding (mpnn.py:89-104): A+ . relu(Z + w_a) + A- . relu(Z - w_a) ----
-  f32x4 ea[4];
-#pragma unroll
-  for (int ft = 0; ft < 4; ++ft) ea[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (has_tile) dense_agg<1>(ea, PL, adjb, kc0, kc1, lane);
-  __syncthreads();
-  if (has_tile) {
-    f32x4 z[4];
-    lin8(z, P + PK_WX, xk0, xk1, lane);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float4 wa = wa_of(c);
-      plane_store4(PL, c, r, s4, valid ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
-                                                     relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
-                                       : zero4());
-    }
-  }
-  __syncthreads();
-  float4 ereg[4];
-  {
-    if (has_tile) dense_agg<2>(ea, PL, adjb, kc0, kc1, lane);
-    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
-    float4 acc[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = make_float4(ea[c][0] / nf, ea[c][1] / nf, ea[c][2] / nf, ea[c][3] / nf);
-    // feature 63 = norm / norm.max()  (mpnn.py:102)
-    const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid ? MD[r / N] : 1);
-    if (s4 == 3) acc[3].w = nf / (float)md;
-    if (!valid) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = zero4();
-    } else if (SAVE) {
-      float* eap = a.sv + (size_t)SV_EAGG * RT * 64 + (R0 + r) * 64 + 4 * s4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st4(eap + 16 * c, acc[c]);
-    }
-    f32x4 d[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) mm_bf3(d, acc, WP, lane);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      ereg[nt] = relu4(d[nt]);
-      if (SAVE && valid) st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r) * 64 + 16 * nt + 4 * s4, ereg[nt]);
-    }
-    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_E, pos_mask(ereg));
-  }
-  __syncthreads();  // every wave is done with the V planes and with Wf
-  ECO_TS(3);
-
-  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55), f32 MFMA per tile, kept in registers + planes ----
-  float4 hreg[4];
-  {
-    f32x4 z[4];
-    lin8(z, P + PK_W0, xk0, xk1, lane);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      hreg[c] = valid ? relu4(z[c]) : zero4();
-      if (has_tile) plane_store4(PL, c, r, s4, hreg[c]);
-      if (SAVE && valid) st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
-    }
-  }
-  if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H0, pos_mask(hreg));
-  __syncthreads();
-  ECO_TS(4);
-
-  // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
-  // per layer: [planes h_l ready] DMA Wm -> WP and Wu(h-half) -> WX | aggregation MFMAs | [B1] message |
-  //            [B2] DMA Wu(m-half) -> WP | Wu(h-half).h | [B3] Wu(m-half).m, h' planes | [next layer]
-  for (int layer = 0; layer < 3; ++layer) {
-    const uint16_t* Wmb = PB + BF_LAYER + layer * BF_LAYER_STRIDE;
-    const uint16_t* Wub = Wmb + 2 * BF_HALF;
-    glds_frags<NW>(WP, Wmb, 48, w, lane);
-    glds_frags<NW>(WX, Wub, 24, w, lane);
-    f32x4 ag[4];
-#pragma unroll
-    for (int ft = 0; ft < 4; ++ft) ag[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) dense_agg<0>(ag, PL, adjb, kc0, kc1, lane);
-    float4 agg[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) agg[c] = make_float4(ag[c][0] / nf, ag[c][1] / nf, ag[c][2] / nf, ag[c][3] / nf);
-    if (SAVE && valid) {
-      float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[c]);
-    }
-    glds_wait();
-    __syncthreads();  // B1: Wm and Wu(h-half) landed
-    // message = relu(Wm . [agg, e])
-    f32x4 d[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) {
-      mm_bf3(d, ereg, WP + BF_HALF, lane);
-      mm_bf3(d, agg, WP, lane);
-    }
-    float4 mrel[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) mrel[c] = relu4(d[c]);
-    if (SAVE && valid) {
-      float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r) * 64 + 4 * s4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[c]);
-      store_mask(a, RT, R0 + r, s4, SM_M0 + layer, pos_mask(mrel));
-    }
-    __syncthreads();  // B2: all waves done with Wm and with the planes of h_layer
-    glds_frags<NW>(WP, Wub + BF_HALF, 24, w, lane);
-    // h' = relu(Wu . [h, m]): the h half while the m half lands
-    f32x4 hn[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) hn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (has_tile) mm_bf3(hn, hreg, WX, lane);
-    glds_wait();
-    __syncthreads();  // B3
-    if (has_tile) mm_bf3(hn, mrel, WP, lane);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      hreg[c] = valid ? relu4(hn[c]) : zero4();
-      if (SAVE && valid) st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r) * 64 + 16 * c + 4 * s4, hreg[c]);
-    }
-    if (SAVE && valid) store_mask(a, RT, R0 + r, s4, SM_H1 + layer, pos_mask(hreg));
-    if (layer < 2 && has_tile) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) plane_store4(PL, c, r, s4, hreg[c]);
-    }
-    __syncthreads();  // planes of h_{layer+1} complete; WP and WX free
-    ECO_TS(5 + layer);
-  }
-
-  // ---- phase E: readout + act over h3 rows staged as fp32 [rows][LDH] in the plane buffer ----
-  float* Hs = lds;
-  if (has_tile) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) st4(Hs + r * LDH + 16 * c + 4 * s4, hreg[c]);
-  }
-  __syncthreads();
-  float* Scr = reinterpret_cast<float*>(WP);
-  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= DN_WP_BYTES;
-  readout_act<SAVE, NW>(a, Hs, LDH, Scr, split, blk, g_valid, rows_valid, R0, RT);
-  ECO_TS(8);
-}
-
-// ============================================================== backward ====
-// Autograd of mpnn_forward_dense_kernel (dqn.py:440-449) for the same blocks: every A^T product is the
-// dense aggregation of the forward (A symmetric), every Linear a transposed bf16x3 product (BFT_*
-// fragments).  Writes the pre-activation gradients the weight-gradient reduction reads (GR_DUU*, GR_DUM*,
-// GR_DUE, GR_DU0, GR_DZ) and the per-graph / per-block partials of the CSR backward; dh and de stay in
-// registers (no GR_DE / GR_DH round trips), and the forward's ReLU decisions come from 16-bit masks it
-// saved (SM_*) instead of re-reading the f32 activation rows.  NW waves own MAXT 16-node tiles each
-// (t = w + ti NW).
-// LDS: PL planes of the gathered gradient G (readout scratch first) | WP 48 fragments | WX 24 fragments |
-//      RI [rows_pad] int2 | GB [gpb] i64
-template <int NW, int MAXT>
-__global__ __launch_bounds__(64 * NW, 1) void mpnn_backward_dense_kernel(MpnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  ECO_TS(16);
-  constexpr int NT = 64 * NW;
-  const int lane = threadIdx.x & 63;
-  const int w = uniform_i(threadIdx.x >> 6);
-  const int blk = blockIdx.x;
-  const int N = a.N;
-  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
-  const int rows_valid = g_valid * N;
-  const int rows_pad = (a.gpb * N + 15) & ~15;
-  const int ntiles = rows_pad >> 4;
-  uint16_t* PL = reinterpret_cast<uint16_t*>(lds);
-  uint32_t* ADJ = reinterpret_cast<uint32_t*>(lds);
-  uint16_t* WP = PL + 3 * DN_PLANE;
-  uint16_t* WX = WP + 2 * BF_HALF;
-  int2* RI = reinterpret_cast<int2*>(WX + BF_HALF);
-  int64_t* GB = reinterpret_cast<int64_t*>(RI + rows_pad);
-  const size_t R0 = (size_t)blk * a.gpb * N;
-  const size_t RT = (size_t)a.B * N;
-  const float* P = a.P;
-  const uint16_t* PB = reinterpret_cast<const uint16_t*>(P + PK_BF);
-  const float* sv = a.sv;
-  float* gr = a.gr;
-  const int s4 = lane >> 4;
-  const int c16 = lane & 15;
-  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
-  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
-  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
-  const float* PP = MEAN + (size_t)a.B * 64;
-  float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
-  float* DWRA = DP + (size_t)a.B * 64;
-  float* DWRB = DWRA + (size_t)a.B * 64;
-  float* DBR = DWRB + (size_t)a.B * 64;
-  float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
-
-  // ---- staging: layer-2 transposed weights (LDS-DMA), row info, edge bases ----
-  glds_frags<NW>(WP, PB + BFT_LAYER + 2 * BF_LAYER_STRIDE + 2 * BF_HALF, 48, w, lane);  // Wu^T
-  glds_frags<NW>(WX, PB + BFT_LAYER + 2 * BF_LAYER_STRIDE, 24, w, lane);                // Wm^T (dagg half)
-  for (int r = threadIdx.x; r < rows_pad; r += NT) RI[r] = pack_row_info(a, blk, r, rows_valid);
-  for (int gl = threadIdx.x; gl < g_valid; gl += NT) GB[gl] = a.gs.edge_base[a.gids[blk * a.gpb + gl]];
-  __syncthreads();
-  // per tile: node, validity, norm, k-chunk range, adjacency bits
-  bool has_tile[MAXT], valid[MAXT];
-  int rw[MAXT], rr[MAXT], kc0[MAXT], kc1[MAXT];
-  float nf[MAXT];
-  uint32_t adjb[MAXT][4];
-  uint4 rmask[MAXT];  // the forward's ReLU masks of this lane's node (SM_* tensors, 16 bits each)
-  {
-    const bool built = adj_build<NT>(a, ADJ, RI, GB, rows_pad, rows_valid);
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      const int t = w + ti * NW;
-      has_tile[ti] = t < ntiles;
-      rw[ti] = t * 16 + c16;
-      valid[ti] = has_tile[ti] && rw[ti] < rows_valid;
-      rr[ti] = min(rw[ti], rows_pad - 1);
-      nf[ti] = (float)row_info(RI, rr[ti]).norm;
-      const int g_lo = min(t * 16, rows_pad - 1) / N, g_hi = min(t * 16 + 15, rows_pad - 1) / N;
-      kc0[ti] = (g_lo * N) >> 5;
-      kc1[ti] = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
-      adj_lane(a, ADJ, built, blk, rw[ti], rr[ti], valid[ti], s4, adjb[ti]);
-      const uint16_t* M = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
-      rmask[ti] = valid[ti] ? *reinterpret_cast<const uint4*>(M + ((R0 + rw[ti]) * 4 + s4) * SM_TENSORS)
-                            : make_uint4(0u, 0u, 0u, 0u);
-    }
-    if (built) __syncthreads();
-  }
-  ECO_TS(17);
-
-  // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
-  float* DQ = lds;                       // [rows_pad]
-  float* DMEAN = DQ + rows_pad;          // [gpb][64]
-  float* RED = DMEAN + a.gpb * 64;       // [gpb][NW][64] (split) or [NW][64]
-  const bool split = a.gpb < NW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * NW * 64) * 4 <= (size_t)DN_PL_BYTES;
-  for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
-  __syncthreads();
-  if (split) {  // dWr[64:] = sum_v dq_v h3_v, spread over all waves
-    for (int gl = 0; gl < g_valid; ++gl) {
-      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
-      float dwb = 0.f;
-      for (int v = w; v < N; v += NW) {
-        const float dv = DQ[gl * N + v];
-        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
-      }
-      RED[(gl * NW + w) * 64 + lane] = dwb;
-    }
-    __syncthreads();
-  }
-  for (int gl = w; gl < g_valid; gl += NW) {
-    const int e = blk * a.gpb + gl;
-    float sacc = 0.f;
-    for (int v = lane; v < N; v += 64) sacc += DQ[gl * N + v];
-    const float S = wave_sum_f(sacc);
-    const float p = PP[(size_t)e * 64 + lane];
-    const float dp = P[PK_WR + lane] * S * (p > 0.f ? 1.f : 0.f);
-    DP[(size_t)e * 64 + lane] = dp;
-    DWRA[(size_t)e * 64 + lane] = relu(p) * S;
-    if (lane == 0) DBR[e] = S;
-    float dmean = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < 64; ++k) dmean = fmaf(P[PK_WP + k * 64 + lane], __shfl(dp, k, 64), dmean);
-    DMEAN[gl * 64 + lane] = dmean / (float)N;
-    float dwb = 0.f;
-    if (split) {
-#pragma unroll
-      for (int k = 0; k < NW; ++k) dwb += RED[(gl * NW + k) * 64 + lane];  // fixed order
-    } else {
-      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
-      for (int v = 0; v < N; ++v) {
-        const float dv = DQ[gl * N + v];
-        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
-      }
-    }
-    DWRB[(size_t)e * 64 + lane] = dwb;
-  }
-  __syncthreads();
-  // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
-  float4 dh[MAXT][4];
-#pragma unroll
-  for (int ti = 0; ti < MAXT; ++ti) {
-    const float dqi = valid[ti] ? DQ[rw[ti]] : 0.f;
-    const int gl = rr[ti] / N;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int f = 16 * c + 4 * s4;
-      const float4 dm = valid[ti] ? f4(DMEAN + gl * 64 + f) : zero4();
-      dh[ti][c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
-                              fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
-    }
-  }
-  __syncthreads();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes (0 * garbage = NaN)
-  {
-    const int KP = (rows_pad + 31) & ~31;
-    const int pad = KP - rows_pad;  // 0 or 16 rows
-    for (int i = threadIdx.x; i < 3 * 4 * pad * 8; i += NT) {  // 8 dwords per 32-B row
-      const int pf = i / (pad * 8), rem = i - pf * (pad * 8);
-      reinterpret_cast<uint32_t*>(PL + (pf >> 2) * DN_PLANE + (pf & 3) * (DN_KPMAX * 16) + rows_pad * 16)[rem] = 0u;
-    }
-  }
-  ECO_TS(18);
-
-  // ---- update layers in reverse (mpnn.py:114-120) ----
-  // [B0: Wu^T in WP, Wm^T(dagg half) in WX; planes free] dh_direct, dm | [B1] DMA Wm^T(de half) -> WP;
-  // dagg -> G planes | [B2] de; DMA next Wm^T(dagg half) -> WX; dh = dh_direct + A.G | [B3] DMA next Wu^T -> WP
-  float4 de[MAXT][4];
-#pragma unroll
-  for (int ti = 0; ti < MAXT; ++ti)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) de[ti][c] = zero4();
-  for (int layer = 2; layer >= 0; --layer) {
-    const uint16_t* WmT = PB + BFT_LAYER + layer * BF_LAYER_STRIDE;
-    // duu = dh' * [h' > 0]  (in place in dh), m > 0 masks
-    uint32_t mmask[MAXT];
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
-      mmask[ti] = mask16(rmask[ti], SM_M0 + layer);
-      const uint32_t hmask = mask16(rmask[ti], SM_H0 + layer + 1);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        dh[ti][c] = masked(f32x4{dh[ti][c].x, dh[ti][c].y, dh[ti][c].z, dh[ti][c].w}, hmask, c);
-        if (valid[ti]) st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[ti][c]);
-      }
-    }
-    if (layer == 1) ECO_TS(24);
-    glds_wait();
-    __syncthreads();  // B0
-    if (layer == 1) ECO_TS(25);
-    // [dh_direct, dm] = Wu^T . duu;  dum = dm * [m > 0]
-    f32x4 dhd[MAXT][4];
-    float4 dum[MAXT][4];
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      f32x4 dmm[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        dhd[ti][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dmm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      if (has_tile[ti]) mm_bf3x2(dhd[ti], dmm, dh[ti], WP, WP + BF_HALF, lane);
-      const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        dum[ti][c] = masked(dmm[c], mmask[ti], c);
-        if (valid[ti]) st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[ti][c]);
-      }
-    }
-    if (layer == 1) ECO_TS(26);
-    __syncthreads();  // B1: WP free
-    if (layer == 1) ECO_TS(27);
-    glds_frags<NW>(WP, WmT + BF_HALF, 24, w, lane);  // Wm^T, de half
-    // dagg = Wm^T(agg half) . dum;  G = dagg / norm (d agg / d(A.h) = 1/norm) -> planes
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      if (!has_tile[ti]) continue;  // wave-uniform
-      f32x4 dg[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mm_bf3(dg, dum[ti], WX, lane);
-      const float n_ = nf[ti];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        plane_store4(PL, c, rw[ti], s4,
-                     valid[ti] ? make_float4(dg[c][0] / n_, dg[c][1] / n_, dg[c][2] / n_, dg[c][3] / n_) : zero4());
-    }
-    if (layer == 1) ECO_TS(28);
-    glds_wait();
-    __syncthreads();  // B2: G planes complete, Wm^T de half landed, WX free
-    if (layer == 1) ECO_TS(29);
-    if (layer > 0) glds_frags<NW>(WX, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE, 24, w, lane);
-    else glds_frags<NW>(WX, PB + BFT_WF, 24, w, lane);  // Wf^T for the edge layer
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      f32x4 dd[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) dd[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (has_tile[ti]) mm_bf3(dd, dum[ti], WP, lane);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        de[ti][c].x += dd[c][0]; de[ti][c].y += dd[c][1]; de[ti][c].z += dd[c][2]; de[ti][c].w += dd[c][3];
-      }
-      // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
-      if (has_tile[ti]) dense_agg<0>(dhd[ti], PL, adjb[ti], kc0[ti], kc1[ti], lane);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) dh[ti][c] = valid[ti] ? as_f4(dhd[ti][c]) : zero4();
-    }
-    if (layer == 1) ECO_TS(30);
-    __syncthreads();  // B3: WP and the planes free
-    if (layer > 0) glds_frags<NW>(WP, PB + BFT_LAYER + (layer - 1) * BF_LAYER_STRIDE + 2 * BF_HALF, 48, w, lane);
-    ECO_TS(21 - layer);
-  }
-
-  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
-  glds_wait();
-  __syncthreads();  // Wf^T landed
-#pragma unroll
-  for (int ti = 0; ti < MAXT; ++ti) {
-    const size_t ro = (R0 + rr[ti]) * 64 + 4 * s4;
-    float4 due[4];
-    const uint32_t h0m = mask16(rmask[ti], SM_H0), em = mask16(rmask[ti], SM_E);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (valid[ti])
-        st4(GR(GR_DU0) + ro + 16 * c, masked(f32x4{dh[ti][c].x, dh[ti][c].y, dh[ti][c].z, dh[ti][c].w}, h0m, c));
-      due[c] = masked(f32x4{de[ti][c].x, de[ti][c].y, de[ti][c].z, de[ti][c].w}, em, c);
-      if (valid[ti]) st4(GR(GR_DUE) + ro + 16 * c, due[c]);
-    }
-    if (has_tile[ti]) {
-      f32x4 dg[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) dg[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mm_bf3(dg, due, WX, lane);
-      const float n_ = nf[ti];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        plane_store4(PL, c, rw[ti], s4,
-                     valid[ti] ? make_float4(dg[c][0] / n_, dg[c][1] / n_, dg[c][2] / n_, dg[c][3] / n_) : zero4());
-    }
-  }
-  __syncthreads();
-  ECO_TS(22);
-  // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
-  {
-    float dwacc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dwacc[i] = 0.f;
-#pragma unroll
-    for (int ti = 0; ti < MAXT; ++ti) {
-      f32x4 gp[4], gm[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        gp[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gm[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      if (has_tile[ti]) {
-        dense_agg<1>(gp, PL, adjb[ti], kc0[ti], kc1[ti], lane);
-        dense_agg<2>(gm, PL, adjb[ti], kc0[ti], kc1[ti], lane);
-      }
-      float xk0 = 0.f, xk1 = 0.f;
-      if (valid[ti]) {
-        xk0 = a.x[(R0 + rw[ti]) * 8 + s4];
-        xk1 = a.x[(R0 + rw[ti]) * 8 + 4 + s4];
-      }
-      f32x4 zz[4];
-      lin8(zz, P + PK_WX, xk0, xk1, lane);  // Z exactly as the forward computed it
-#ifdef ECO_DBG_VALU_Z
-      {
-        float4 x0 = zero4(), x1 = zero4();
-        if (valid[ti]) { x0 = f4(a.x + (R0 + rw[ti]) * 8); x1 = f4(a.x + (R0 + rw[ti]) * 8 + 4); }
-        for (int c = 0; c < 4; ++c) for (int i = 0; i < 4; ++i) {
-          const int f = 16 * c + 4 * s4 + i;
-          const float4 w0 = f4(P + PK_WX + f * 8), w1 = f4(P + PK_WX + f * 8 + 4);
-          zz[c][i] = w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w + w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
-        }
-      }
-#endif
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float dz4[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int f = 16 * c + 4 * s4 + i;
-          const float z = zz[c][i];
-          const float wa = P[PK_WA + f];
-          const float tp = fmaf(1.f, wa, z) > 0.f ? gp[c][i] : 0.f;
-          const float tm = fmaf(-1.f, wa, z) > 0.f ? gm[c][i] : 0.f;
-          dz4[i] = valid[ti] ? tp + tm : 0.f;
-          dwacc[4 * c + i] += valid[ti] ? tp - tm : 0.f;
-        }
-        if (valid[ti])
-          st4(GR(GR_DZ) + (R0 + rw[ti]) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
-      }
-    }
-    // reduce dw_a over the 16 node lanes sharing s4, then over waves (fixed order)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float v = dwacc[i];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      dwacc[i] = v;
-    }
-    __syncthreads();  // every wave is done reading the G planes: the region becomes the dwa scratch
-    float* REDW = lds;  // [NW][64]
-    if (c16 == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        st4(REDW + w * 64 + 16 * c + 4 * s4,
-            make_float4(dwacc[4 * c], dwacc[4 * c + 1], dwacc[4 * c + 2], dwacc[4 * c + 3]));
-    }
-    __syncthreads();
-    if (w == 0) {
-      float sacc = 0.f;
-#pragma unroll
-      for (int k = 0; k < NW; ++k) sacc += REDW[k * 64 + lane];
-      DWA[(size_t)blk * 64 + lane] = sacc;
-    }
-  }
-  ECO_TS(23);
-}
-
-static int mpnn_backward_dense_launch(const MpnnArgs& a, hipStream_t st) {
-  const int rows_pad = (a.gpb * a.N + 15) & ~15;
-  const size_t lds = dense_fwd_lds_bytes(rows_pad, a.gpb);
-  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
-  const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  // 16 waves x 1 tile (latency hiding; 2 VGPRs spill) is faster than 8 x 2 (no spills): 0.70 vs 0.82 ms
-  // at M=2048 ER-200.
-  if (true) {
-    (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel<16, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_backward_dense_kernel<16, 1><<<blocks, 1024, lds, st>>>(a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)mpnn_backward_dense_kernel<8, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_backward_dense_kernel<8, 2><<<blocks, 512, lds, st>>>(a);
-  }
-  return check_launch("mpnn_backward_dense");
-}
-
-static int mpnn_forward_dense_launch(const MpnnArgs& a, bool save, hipStream_t st) {
-  const int rows_pad = (a.gpb * a.N + 15) & ~15;
-  const size_t lds = dense_fwd_lds_bytes(rows_pad, a.gpb);
-  if (lds > 160 * 1024) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS budget");
-  const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  if (save) {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    mpnn_forward_dense_kernel<true><<<blocks, 64 * DN_NW, lds, st>>>(a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)mpnn_forward_dense_kernel<false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    mpnn_forward_dense_kernel<false><<<blocks, 64 * DN_NW, lds, st>>>(a);
-  }
-  return check_launch("mpnn_forward_dense");
-}
-
-#endif  // ECO_AB_DENSE_V1
 
 }  // namespace eco

@@ -27,9 +27,6 @@
 // instead of four; the edge layer writes the U and V planes at once (V into the two idle weight buffers).
 // Saved activations and ReLU masks have the layout of eco_mpnn_dense.h (the backward reads them unchanged).
 #pragma once
-#ifndef D2B_EARLY_X
-#define D2B_EARLY_X 0  // A/B knob (backward): see the dz phase
-#endif
 #include "eco_mpnn_dense.h"
 
 namespace eco {
@@ -983,15 +980,6 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
   }
 
   // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
-#if D2B_EARLY_X  // A/B: the inputs of Z recomputed below, loaded before the Wf^T product
-  float xk0 = 0.f, xk1 = 0.f;
-  if (valid) {
-    xk0 = a.x[(R0 + rw) * 8 + s4];
-    xk1 = a.x[(R0 + rw) * 8 + 4 + s4];
-  }
-  float wx8[8];
-  lin8_load(P + PK_WX, lane, wx8);
-#endif
   glds_wait();
   lds_barrier();  // Wf^T landed
   {
@@ -1023,7 +1011,6 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     float dwacc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwacc[i] = 0.f;
-#if !D2B_EARLY_X
     float xk0 = 0.f, xk1 = 0.f;  // inputs of Z, loaded ahead of the aggregations
     if (valid) {
       xk0 = a.x[(R0 + rw) * 8 + s4];
@@ -1031,7 +1018,6 @@ __global__ __launch_bounds__(64 * DN_NW, 1) void mpnn_backward_dense2_kernel(Mpn
     }
     float wx8[8];
     lin8_load(P + PK_WX, lane, wx8);
-#endif
     float4 wa4[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);

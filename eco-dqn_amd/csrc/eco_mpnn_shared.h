@@ -37,9 +37,6 @@ namespace eco {
 #ifndef SH_NW_X
 #define SH_NW_X 16
 #endif
-#ifndef ECO_AB_SHARED_BF3
-#define ECO_AB_SHARED_BF3 0            // A/B builds only (tools/): the round-3 six-product bf16x3 Linears
-#endif
 constexpr int SH_EPS = 4;              // episodes per slice
 constexpr int SH_NPT = 16 / SH_EPS;    // nodes per Linear tile: 16 MFMA rows = SH_NPT nodes x SH_EPS episodes
 constexpr int SH_NW = SH_NW_X;         // waves per Linear workgroup (one workgroup per CU: <= 128 VGPRs at 16)
@@ -665,15 +662,9 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
   const int c16 = lane & 15, s4 = lane >> 4;
   const int kn = c16 / SH_EPS, eps = c16 % SH_EPS;
   uint16_t* WL = reinterpret_cast<uint16_t*>(lds);
-#if ECO_AB_SHARED_BF3  // A/B builds only: the six-product bf16x3 Linears (Wf 24 fragments, Wm + Wu 96)
-  const uint16_t* PB = reinterpret_cast<const uint16_t*>(a.P + PK_BF);
-  if (PHASE == 0) glds_frags<SH_NW>(WL, PB + BF_WF, 24, w, lane);
-  else glds_frags<SH_NW>(WL, PB + BF_LAYER + layer * BF_LAYER_STRIDE, 96, w, lane);
-#else  // fp16x2 pieces (PK_FH): Wf 16 fragments, Wm + Wu of the layer 64 (four 64-input halves)
   const uint16_t* PH = reinterpret_cast<const uint16_t*>(a.P + PK_FH);
   if (PHASE == 0) glds_frags<SH_NW>(WL, PH + FH_WF, 16, w, lane);
   else glds_frags<SH_NW>(WL, PH + FH_LAYER + layer * FH_LAYER_STRIDE, 64, w, lane);
-#endif
   const int N = a.N;
   const int gid = a.gids[0];
   const float* P = a.P;
@@ -742,13 +733,9 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#if ECO_AB_SHARED_BF3
-      mm_bf3_seq(d, acc, WL, lane);
-#else
       const int kx = node_exp<4>(acc);
       mm_fh_seq(d, acc, exp2i(kx), WL, lane);
       unscale(d, kx + fh_kw(P, 0));
-#endif
       if (nvalid) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) st4_nt(sb.EB + ro + nt * cs, rvalid ? relu4(d[nt]) : zero4());
@@ -757,10 +744,6 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
       f32x4 d[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) d[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#if ECO_AB_SHARED_BF3
-      mm_bf3_seq(d, acc, WL, lane);               // message = relu(Wm . [agg, e])
-      mm_bf3_seq(d, cu.ev, WL + BF_HALF, lane);
-#else
       {  // message = relu(Wm . [agg, e]): one node scale over both halves, as the dense kernels
         const int kx = node_exp2(acc, cu.ev);
         const float sf = exp2i(kx);
@@ -768,7 +751,6 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
         mm_fh_seq(d, acc, sf, WL, lane);
         unscale(d, kx + fh_kw(P, 1 + 2 * layer));
       }
-#endif
       float4 mr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) mr[c] = relu4(d[c]);
@@ -785,10 +767,6 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
 #pragma unroll
         for (int c = 0; c < 4; ++c) hc[c] = relu4(z[c]);
       }
-#if ECO_AB_SHARED_BF3
-      mm_bf3_seq(hn, hc, WL + 2 * BF_HALF, lane);  // h' = relu(Wu . [h, m])
-      mm_bf3_seq(hn, mr, WL + 3 * BF_HALF, lane);
-#else
       {  // h' = relu(Wu . [h, m])
         const int kx = node_exp2(hc, mr);
         const float sf = exp2i(kx);
@@ -796,7 +774,6 @@ __global__ __launch_bounds__(64 * SH_NW, 1) void shared_lin_kernel(MpnnArgs a, S
         mm_fh_seq(hn, mr, sf, WL + 3 * FH_HALF, lane);
         unscale(hn, kx + fh_kw(P, 2 + 2 * layer));
       }
-#endif
       if (PHASE == 1) {
         if (nvalid) {
 #pragma unroll
@@ -928,9 +905,6 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   SharedBufs sb = shared_carve((float*)((char*)workspace + 256), a.N, a.B);
   uint64_t* key = reinterpret_cast<uint64_t*>((char*)workspace + WS_KEY_OFFSET);
   sb.key = key;
-#if ECO_AB_SHARED_NO_CACHE  // A/B builds only (tools/): rebuild the tables every call
-  (void)hipMemsetAsync(key, 0xFF, 2 * sizeof(uint64_t), st);
-#endif
   shared_key_kernel<<<1, SK_THREADS, 0, st>>>(a, key);
   shared_perm_kernel<<<(a.N + 63) / 64, 256, 0, st>>>(a, sb);
   shared_tiles_kernel<<<(sb.nt16 * 2 + ST_THREADS - 1) / ST_THREADS, ST_THREADS, 0, st>>>(a, sb);
@@ -943,11 +917,7 @@ static int mpnn_forward_shared_launch(const MpnnArgs& a, void* workspace, hipStr
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   (void)hipFuncSetAttribute((const void*)shared_agg_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_agg);
   const int grid = shared_grid();
-#if ECO_AB_SHARED_BF3
-  const size_t lds_edge = 24 * BF_FRAG * 2, lds_layer = 96 * BF_FRAG * 2;
-#else
   const size_t lds_edge = 16 * FH_FRAG * 2, lds_layer = 64 * FH_FRAG * 2;
-#endif
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_edge);
   (void)hipFuncSetAttribute((const void*)shared_lin_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -23,146 +23,19 @@ struct WJob {
   int out_col0;      // first column in the flat buffer
 };
 constexpr int MAX_JOBS = 10;
-#ifndef WGRAD_SWZ
-#define WGRAD_SWZ 0  // A/B knob: wgrad_bf3 planes without padding (XOR-swizzled 16-B chunks): 37 KB, 4 per CU
-#endif
-#ifndef WGRAD_WG_X
-#if WGRAD_SWZ
-#define WGRAD_WG_X 4
-#else
-#define WGRAD_WG_X 3  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
-#endif
-#endif
-// Compile-time A/B variants (tools/ builds only; the product library has exactly one weight-gradient path)
-#ifndef ECO_AB_WGRAD_F32
-#define ECO_AB_WGRAD_F32 0  // wgrad_kernel: the f32-MFMA reduction
-#endif
-#ifndef ECO_AB_WGRAD_FH
-#define ECO_AB_WGRAD_FH 0  // wgrad_fh_kernel: the fp16x2 reduction
-#endif
-#ifndef WGRAD_FH_WG_X
-#define WGRAD_FH_WG_X 3  // wgrad_fh_kernel: workgroups per CU over all jobs (27 KB LDS each)
-#endif
-#ifndef WGRAD_FH_WAVES
-#define WGRAD_FH_WAVES 3  // wgrad_fh_kernel: register budget for this many waves per SIMD
-#endif
+constexpr int WGRAD_WG_X = 3;  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
 constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
 constexpr int SLAB = 64 * 128;
 constexpr int WROWS = 32;                  // rows per LDS tile
-#if ECO_AB_WGRAD_F32
-constexpr int LDY = 68, LDX = 132;         // padded LDS row strides (wgrad_kernel)
-#endif
 
 struct WJobs {
   WJob j[MAX_JOBS];
   int n;
-  int nwg;  // workgroups (= slabs) per job, <= WG_PER_JOB (wgrad_kernel: every job)
   int nwgj[MAX_JOBS];     // wgrad_bf3_kernel / reduce: workgroups (= slabs) of job j, <= WG_PER_JOB
   int first[MAX_JOBS + 1];  // wgrad_bf3_kernel: first flat block of job j (1-D grid of first[n] blocks)
 };
 
-#if ECO_AB_WGRAD_F32
-// One workgroup (4 waves) reduces a contiguous row range of one job: 32-row tiles of dY and
-// X are staged in LDS with 16-byte coalesced loads; each wave owns up to two 32x32 output
-// tiles (o-tile, i-tile) and runs v_mfma_f32_32x32x2_f32 over the rows (k = row pair).
-__global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
-  __shared__ __attribute__((aligned(16))) float sY[WROWS * LDY];
-  __shared__ __attribute__((aligned(16))) float sX[WROWS * LDX];
-  const WJob& J = jobs.j[blockIdx.y];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int jj = lane & 31, h = lane >> 5;
-  const int K = J.K1 + J.K2;
-  const int K4 = (K + 3) & ~3;
-  const int ntile = 2 * ((K + 31) / 32);
-  const int chunk = ((J.R + jobs.nwg - 1) / jobs.nwg + WROWS - 1) / WROWS * WROWS;
-  const int r0 = blockIdx.x * chunk;
-  const int r1 = min(J.R, r0 + chunk);
-  f32x16 acc[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
-  // register double-buffering: tile rb + 32 is loaded while tile rb's MFMAs run
-  const int per = K4 >> 2;
-  float4 ry[2], rx[4];
-  auto load_tile = [&](int rb) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = threadIdx.x + 256 * k;  // WROWS * 16 = 512 float4
-      const int r = i >> 4, c = (i & 15) * 4;
-      ry[k] = rb + r < r1 ? *reinterpret_cast<const float4*>(J.dY + (size_t)(rb + r) * 64 + c)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = threadIdx.x + 256 * k;  // up to WROWS * 32 = 1024 float4
-      rx[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i < WROWS * per) {
-        const int r = i / per, c = (i - r * per) * 4;
-        if (rb + r < r1) {
-          const size_t rr = (size_t)(rb + r);
-          rx[k] = c < J.K1 ? *reinterpret_cast<const float4*>(J.X1 + rr * J.ld1 + c)
-                           : *reinterpret_cast<const float4*>(J.X2 + rr * J.ld2 + (c - J.K1));
-        }
-      }
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = threadIdx.x + 256 * k;
-      *reinterpret_cast<float4*>(sY + (i >> 4) * LDY + (i & 15) * 4) = ry[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = threadIdx.x + 256 * k;
-      if (i < WROWS * per) {
-        const int r = i / per, c = (i - r * per) * 4;
-        *reinterpret_cast<float4*>(sX + r * LDX + c) = rx[k];
-      }
-    }
-  };
-  if (r0 < r1) load_tile(r0);
-  for (int rb = r0; rb < r1; rb += WROWS) {
-    store_tile();
-    __syncthreads();
-    if (rb + WROWS < r1) load_tile(rb + WROWS);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int t = w + 4 * q;
-      if (t < ntile) {
-        const int ot = t & 1, it = t >> 1;
-        const int col = 32 * it + jj;
-        const bool cv = col < K;
-#pragma unroll
-        for (int kk = 0; kk < WROWS / 2; ++kk) {
-          const int r = 2 * kk + h;
-          const float av = sY[r * LDY + 32 * ot + jj];
-          const float bv = cv ? sX[r * LDX + col] : 0.f;
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[q], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  float* slab = slabs + ((size_t)blockIdx.y * SLABS_PER_JOB + blockIdx.x) * SLAB;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int t = w + 4 * q;
-    if (t < ntile) {
-      const int ot = t & 1, it = t >> 1;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
-        slab[o * 128 + 32 * it + jj] = acc[q][k];
-      }
-    }
-  }
-}
-
-#endif  // ECO_AB_WGRAD_F32
 
 // Same reduction on 32x32x16 bf16 MFMAs: dY and X are split EXACTLY into three bf16 pieces while a
 // 32-row tile is staged (split3_bits), and the six products above 2^-24 relative are accumulated in
@@ -171,26 +44,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WJobs jobs, float* slabs) {
 // (each wave-level load is one contiguous 256-B row segment), splits, and writes the three 8-row
 // pieces as 16-B LDS stores into [p][column][row] planes, which are exactly the MFMA fragments
 // (lane l: column l & 31, rows 8 (l >> 5) .. +7 of a 16-row k-step).
-#ifndef WGRAD_DEPTH
-#define WGRAD_DEPTH 2  // register buffers per thread in wgrad_bf3_job (A/B knob)
-#endif
-#ifndef WGRAD_NT
-#define WGRAD_NT 0  // A/B knob: nontemporal (streaming) loads of dY / X in wgrad_bf3_job
-#endif
-#if WGRAD_NT
-#define WG_LOAD(p) __builtin_nontemporal_load(p)
-#else
-#define WG_LOAD(p) (*(p))
-#endif
-#if WGRAD_SWZ
-// bf16 per plane column (32 rows, no pad): the 16-B row chunk k of column c is stored at chunk k ^ ((c >> 2) & 3), so
-// the 16 consecutive columns of a 16-lane ds_read / ds_write_b128 group hit 16 distinct 4-bank groups
-constexpr int WB_LD = 32;
-#define WB_CH(k, c) ((k) ^ (((c) >> 2) & 3))
-#else
 constexpr int WB_LD = 40;  // bf16 per plane column (32 rows + 8 pad: 80-B stride, conflict-light 16-B reads)
-#define WB_CH(k, c) (k)
-#endif
 typedef short bf16x8w __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
 
@@ -257,55 +111,46 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
   // time makes the compiler wait for every load before the multiply it should overlap)
   auto load_tile = [&](Regs& R, int rb) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) R.y[k] = WG_LOAD(&ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64]);
+    for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
 #pragma unroll
     for (int u = 0; u < XU; ++u)
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        R.x[u][k] = WG_LOAD(&xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld]);
+        R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld];
   };
   auto store_tile = [&](Regs& R, int rb) {
     asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
 #pragma unroll
     for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
-    split8_store(sY + yc * WB_LD + 8 * WB_CH(yg, yc), PY, R.y);
+    split8_store(sY + yc * WB_LD + 8 * yg, PY, R.y);
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         R.x[u][k] = rb + 8 * (xg0 + XG * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
-      split8_store(sX + xc * WB_LD + 8 * WB_CH(xg0 + XG * u, xc), PX, R.x[u]);
+      split8_store(sX + xc * WB_LD + 8 * (xg0 + XG * u), PX, R.x[u]);
     }
   };
   // this wave's output tiles: t = w + 4q -> o-tile w & 1, i-tiles (w >> 1) and (w >> 1) + 2
   const int ot = w & 1;
   const bool live0 = w < ntile, live1 = w + 4 < ntile;
-#if WGRAD_SWZ
-  // k-step s reads row chunk 2s + h of the lane's column (every column this lane reads has the same (c >> 2) & 3)
-  const int so[2] = {8 * WB_CH(h, jj), 8 * WB_CH(2 + h, jj)};
-  const uint16_t* ya = sY + (32 * ot + jj) * WB_LD;
-  const uint16_t* xb0 = sX + (32 * (w >> 1) + jj) * WB_LD;
-#define WB_OFF(s) so[s]
-#else
   const uint16_t* ya = sY + (32 * ot + jj) * WB_LD + 8 * h;
   const uint16_t* xb0 = sX + (32 * (w >> 1) + jj) * WB_LD + 8 * h;
-#define WB_OFF(s) (16 * (s))
-#endif
   const uint16_t* xb1 = xb0 + 64 * WB_LD;
   auto compute = [&]() {
   if (live0) {
 #pragma unroll
     for (int s = 0; s < WROWS / 16; ++s) {
-      const bf16x8w a1 = *reinterpret_cast<const bf16x8w*>(ya + WB_OFF(s));
-      const bf16x8w a2 = *reinterpret_cast<const bf16x8w*>(ya + PY + WB_OFF(s));
-      const bf16x8w a3 = *reinterpret_cast<const bf16x8w*>(ya + 2 * PY + WB_OFF(s));
-      const bf16x8w b1 = *reinterpret_cast<const bf16x8w*>(xb0 + WB_OFF(s));
-      const bf16x8w b2 = *reinterpret_cast<const bf16x8w*>(xb0 + PX + WB_OFF(s));
-      const bf16x8w b3 = *reinterpret_cast<const bf16x8w*>(xb0 + 2 * PX + WB_OFF(s));
+      const bf16x8w a1 = *reinterpret_cast<const bf16x8w*>(ya + 16 * s);
+      const bf16x8w a2 = *reinterpret_cast<const bf16x8w*>(ya + PY + 16 * s);
+      const bf16x8w a3 = *reinterpret_cast<const bf16x8w*>(ya + 2 * PY + 16 * s);
+      const bf16x8w b1 = *reinterpret_cast<const bf16x8w*>(xb0 + 16 * s);
+      const bf16x8w b2 = *reinterpret_cast<const bf16x8w*>(xb0 + PX + 16 * s);
+      const bf16x8w b3 = *reinterpret_cast<const bf16x8w*>(xb0 + 2 * PX + 16 * s);
       if (live1) {
-        const bf16x8w c1 = *reinterpret_cast<const bf16x8w*>(xb1 + WB_OFF(s));
-        const bf16x8w c2 = *reinterpret_cast<const bf16x8w*>(xb1 + PX + WB_OFF(s));
-        const bf16x8w c3 = *reinterpret_cast<const bf16x8w*>(xb1 + 2 * PX + WB_OFF(s));
+        const bf16x8w c1 = *reinterpret_cast<const bf16x8w*>(xb1 + 16 * s);
+        const bf16x8w c2 = *reinterpret_cast<const bf16x8w*>(xb1 + PX + 16 * s);
+        const bf16x8w c3 = *reinterpret_cast<const bf16x8w*>(xb1 + 2 * PX + 16 * s);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, b1, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a3, c1, acc[1], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b2, acc[0], 0, 0, 0);
@@ -331,7 +176,6 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
   };
   // loads are issued unconditionally (rows past r1 clamp to r1 - 1 and are masked at the store): a
   // conditional load makes the compiler drain every tile in flight at the join (vmcnt(0))
-#if WGRAD_DEPTH == 2
   if (r0 < r1) {
     Regs RA, RB;
     load_tile(RA, r0);
@@ -350,26 +194,6 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
       __syncthreads();
     }
   }
-#else  // A/B: D register buffers (3 and 4 measured slower)
-  if (r0 < r1) {
-    constexpr int D = WGRAD_DEPTH;  // register buffers: tiles i+1 .. i+D-1 in flight while tile i is multiplied
-    Regs RB[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) load_tile(RB[d], r0 + d * WROWS);
-    for (int rb = r0; rb < r1; rb += D * WROWS) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int rt = rb + d * WROWS;
-        if (d > 0 && rt >= r1) break;
-        store_tile(RB[d], rt);
-        __syncthreads();
-        load_tile(RB[d], rt + D * WROWS);
-        compute();
-        __syncthreads();
-      }
-    }
-  }
-#endif
   float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -394,201 +218,6 @@ __global__ __launch_bounds__(256) void wgrad_bf3_kernel(WJobs jobs, float* slabs
   else wgrad_bf3_job<false>(jobs, slabs, jb, sY, sX);
 }
 
-#if ECO_AB_WGRAD_FH
-// Same reduction on fp16x2 operands (eco_mpnn_dense2.h's numerics) and 32x32x16 f16 MFMAs: the 32-row tiles
-// of dY and X are staged in LDS as f32, transposed to [column][row] (stride 36 floats: the 16 lanes of a
-// ds_read_b128 group hit 16 disjoint 4-bank groups) through the same register double buffers.  Each wave
-// then splits its own operand fragments per 16-row k-step: a power-of-two scale per (16 rows x 32 columns)
-// fragment (its wave-wide max |v| into [2^14, 2^15)), v 2^k = hi + lo in fp16 (22 significand bits), the
-// three products hi.hi + hi.lo + lo.hi into a zeroed f32 accumulator, which is added into the running sum
-// scaled back by 2^-(ka + kb).  Against the bf16x3 kernel: half the MFMAs (3 products instead of 6), two
-// fp16 pieces split from registers after the barrier instead of three bf16 planes before it, 27 KB of LDS
-// instead of 46 KB.  Error per product <= ~2^-21 relative, or 2^-40 of the fragment's largest term.
-constexpr int WF_LD = 36;  // f32 per staged column (32 rows + 4 pad)
-typedef _Float16 wf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 wf16x2 __attribute__((ext_vector_type(2)));
-typedef float wf32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t wf_pk(float a, float b) {
-  const wf32x2 v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, wf16x2));
-}
-// eight scaled values -> hi / lo fp16 fragments (v = hi + lo to 2^-22)
-__device__ __forceinline__ void wf_split8(const float4& p, const float4& q, float sf, wf16x8& hi, wf16x8& lo) {
-  const float v[8] = {p.x * sf, p.y * sf, p.z * sf, p.w * sf, q.x * sf, q.y * sf, q.z * sf, q.w * sf};
-  u32x4w h, l;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    h[t] = wf_pk(v[2 * t], v[2 * t + 1]);
-    const wf32x2 back = __builtin_convertvector(__builtin_bit_cast(wf16x2, (uint32_t)h[t]), wf32x2);
-    l[t] = wf_pk(v[2 * t] - back[0], v[2 * t + 1] - back[1]);
-  }
-  hi = __builtin_bit_cast(wf16x8, h);
-  lo = __builtin_bit_cast(wf16x8, l);
-}
-__device__ __forceinline__ float wf_absmax8(const float4& p, const float4& q) {
-  return fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
-               fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
-}
-__device__ __forceinline__ float wf_wave_max(float m) {  // non-negative floats order as ints
-  int v = __float_as_int(m);
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false));  // row_ror:8
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xF, 0xF, false));  // row_ror:4
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x122, 0xF, 0xF, false));  // row_ror:2
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x121, 0xF, 0xF, false));  // row_ror:1
-  auto s16 = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
-  v = max((int)s16[0], (int)s16[1]);
-  auto s32 = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
-  return __int_as_float(max((int)s32[0], (int)s32[1]));
-}
-__device__ __forceinline__ int wf_scale_exp(float mx) {  // max 2^k in [2^14, 2^15); 0 for zero / non-finite
-  if (!(mx > 0.f) || mx == INFINITY) return 0;
-  const int k = 15 - __builtin_amdgcn_frexp_expf(mx);
-  return k < -110 ? -110 : (k > 110 ? 110 : k);
-}
-__device__ __forceinline__ float wf_exp2i(int k) {
-  k = k < -126 ? -126 : (k > 127 ? 127 : k);
-  return __int_as_float((k + 127) << 23);
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGRAD_FH_WAVES, WGRAD_FH_WAVES))) void wgrad_fh_kernel(WJobs jobs, float* slabs) {
-  constexpr int PY = 64 * WF_LD, PX = 128 * WF_LD;
-  __shared__ __attribute__((aligned(16))) float sY[PY];
-  __shared__ __attribute__((aligned(16))) float sX[PX];
-  int jb = 0;
-  while (jb + 1 < jobs.n && (int)blockIdx.x >= jobs.first[jb + 1]) ++jb;
-  const int wg = (int)blockIdx.x - jobs.first[jb], nwg = jobs.nwgj[jb];
-  const WJob& J = jobs.j[jb];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int jj = lane & 31, h = lane >> 5;
-  const int K = J.K1 + J.K2;
-  const int ntile = 2 * ((K + 31) / 32);
-  const int chunk = ((J.R + nwg - 1) / nwg + WROWS - 1) / WROWS * WROWS;
-  const int r0 = wg * chunk;
-  const int r1 = min(J.R, r0 + chunk);
-  const int yc = threadIdx.x & 63, yg = threadIdx.x >> 6;
-  const int xc = threadIdx.x & 127, xg0 = threadIdx.x >> 7;
-  typedef const __attribute__((address_space(1))) float gfloat;
-  const bool xlive = xc < K;
-  gfloat* ysrc = (gfloat*)(J.dY + yc);
-  const float* xsrc = !xlive ? J.X1 : (xc < J.K1 ? J.X1 + xc : J.X2 + (xc - J.K1));
-  int xld = xlive && xc >= J.K1 ? J.ld2 : J.ld1;
-  uint32_t xmask = xlive ? 0xFFFFFFFFu : 0u;
-  asm volatile("" : "+v"(xsrc), "+v"(xld), "+v"(xmask));
-  gfloat* xg = (gfloat*)xsrc;
-  const int rlast = r1 - 1;
-  f32x16 acc[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc[q][k] = 0.f;
-  struct Regs {
-    float y[8], x[2][8];
-  };
-  auto load_tile = [&](Regs& R, int rb) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + 2 * u) + k, rlast) * (size_t)xld];
-  };
-  auto store8 = [&](float* dst, const float (&v)[8]) {
-    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  };
-  auto store_tile = [&](Regs& R, int rb) {
-    asm volatile("" : "+s"(rb));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) R.y[k] = rb + 8 * yg + k < r1 ? R.y[k] : 0.f;
-    store8(sY + yc * WF_LD + 8 * yg, R.y);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        R.x[u][k] = rb + 8 * (xg0 + 2 * u) + k < r1 ? __uint_as_float(__float_as_uint(R.x[u][k]) & xmask) : 0.f;
-      store8(sX + xc * WF_LD + 8 * (xg0 + 2 * u), R.x[u]);
-    }
-  };
-  const int ot = w & 1;
-  const bool live0 = w < ntile, live1 = w + 4 < ntile;
-  const float* ya = sY + (32 * ot + jj) * WF_LD + 8 * h;
-  const float* xb0 = sX + (32 * (w >> 1) + jj) * WF_LD + 8 * h;
-  const float* xb1 = xb0 + 64 * WF_LD;
-  auto compute = [&]() {
-    if (!live0) return;
-#pragma unroll
-    for (int s = 0; s < WROWS / 16; ++s) {
-      const float4 a0 = *reinterpret_cast<const float4*>(ya + 16 * s);
-      const float4 a1 = *reinterpret_cast<const float4*>(ya + 16 * s + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(xb0 + 16 * s);
-      const float4 b1 = *reinterpret_cast<const float4*>(xb0 + 16 * s + 4);
-      float4 c0 = make_float4(0.f, 0.f, 0.f, 0.f), c1 = c0;
-      if (live1) {
-        c0 = *reinterpret_cast<const float4*>(xb1 + 16 * s);
-        c1 = *reinterpret_cast<const float4*>(xb1 + 16 * s + 4);
-      }
-      const int ka = wf_scale_exp(wf_wave_max(wf_absmax8(a0, a1)));
-      const int kb = wf_scale_exp(wf_wave_max(wf_absmax8(b0, b1)));
-      wf16x8 ah, al, bh, bl;
-      wf_split8(a0, a1, wf_exp2i(ka), ah, al);
-      wf_split8(b0, b1, wf_exp2i(kb), bh, bl);
-      f32x16 t = {};
-      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, t, 0, 0, 0);
-      const float ub = wf_exp2i(-(ka + kb));
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc[0][k] = fmaf(t[k], ub, acc[0][k]);
-      if (live1) {
-        const int kc = wf_scale_exp(wf_wave_max(wf_absmax8(c0, c1)));
-        wf16x8 ch, cl;
-        wf_split8(c0, c1, wf_exp2i(kc), ch, cl);
-        f32x16 u = {};
-        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch, u, 0, 0, 0);
-        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl, u, 0, 0, 0);
-        u = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch, u, 0, 0, 0);
-        const float uc = wf_exp2i(-(ka + kc));
-#pragma unroll
-        for (int k = 0; k < 16; ++k) acc[1][k] = fmaf(u[k], uc, acc[1][k]);
-      }
-    }
-  };
-  if (r0 < r1) {
-    constexpr int D = WGRAD_DEPTH;  // register buffers: tiles i+1 .. i+D-1 in flight while tile i is multiplied
-    Regs RB[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) load_tile(RB[d], r0 + d * WROWS);
-    for (int rb = r0; rb < r1; rb += D * WROWS) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int rt = rb + d * WROWS;
-        if (d > 0 && rt >= r1) break;
-        store_tile(RB[d], rt);
-        __syncthreads();
-        load_tile(RB[d], rt + D * WROWS);
-        compute();
-        __syncthreads();
-      }
-    }
-  }
-  float* slab = slabs + ((size_t)jb * SLABS_PER_JOB + wg) * SLAB;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int t = w + 4 * q;
-    if (t < ntile) {
-      const int it = t >> 1;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int o = 32 * ot + (k & 3) + 8 * (k >> 2) + 4 * h;  // 32x32 C/D layout
-        slab[o * 128 + 32 * it + jj] = acc[q][k];
-      }
-    }
-  }
-}
-
-#endif  // ECO_AB_WGRAD_FH
 
 // fixed-order sum of the slabs of every job into the flat gradient
 __global__ void wgrad_reduce_kernel(WJobs jobs, const float* slabs, float* grad) {
@@ -1022,20 +651,15 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
   J.j[n++] = WJob{GR(GR_DZ), obs_x, nullptr, xw, n_obs_in, 0, 0, R, 63, fo.We, 1 + n_obs_in, 1};
   J.j[n++] = WJob{DP, MEAN, nullptr, 64, 64, 0, 0, batch, 64, fo.Wp, 64, 0};
   J.n = n;
-#if ECO_AB_WGRAD_F32  // A/B builds only (tools/): the f32-MFMA reduction
-  J.nwg = WG_PER_JOB;
-  for (int j = 0; j < n; ++j) J.nwgj[j] = WG_PER_JOB;
-  wgrad_kernel<<<dim3(J.nwg, n), 256, 0, st>>>(J, slabs);
-#else
   {
     // one resident wave of workgroups over the 256 CUs (46 KB LDS: 3 per CU for bf16x3; 27 KB and 168 VGPRs:
     // 3 per CU for fp16x2).  Measured splits (M = 2048 ER-200): in proportion to the bytes each job reads,
     // 1.28 vs 1.05 ms per gradient step of backward + weight gradients against an even split; more workgroups
     // for the K = 128 jobs at the others' expense (96 / 112 each) slower again (9.25 / 12.1 vs 8.66 ms
-    // per vector step): the K <= 64 jobs cost as much per row.  The fp16x2 kernel (ECO_AB_WGRAD_FH builds)
+    // per vector step): the K <= 64 jobs cost as much per row.  The fp16x2 variant (round 3)
     // measured 0.62 vs 0.52 ms per launch: its per-fragment scales and splits sit after the barrier, on the
     // critical path.
-    const int total = (ECO_AB_WGRAD_FH ? WGRAD_FH_WG_X : WGRAD_WG_X) * 256;
+    const int total = WGRAD_WG_X * 256;
     double rows = 0.0;
     for (int j = 0; j < n; ++j) rows += J.j[j].R;
     J.first[0] = 0;
@@ -1046,13 +670,8 @@ extern "C" int eco_mpnn_backward(const float* packed, int32_t n_obs_in, const ec
       J.nwgj[j] = std::max(1, std::min(WG_PER_JOB, g));
       J.first[j + 1] = J.first[j] + J.nwgj[j];
     }
-#if ECO_AB_WGRAD_FH
-    wgrad_fh_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
-#else
     wgrad_bf3_kernel<<<J.first[n], 256, 0, st>>>(J, slabs);
-#endif
   }
-#endif
   wgrad_reduce_kernel<<<dim3(64 * 128 / 256, n), 256, 0, st>>>(J, slabs, grad);
   ColJobs CJ{};
   CJ.j[0] = ColJob{DWRA, batch, 64, 64, grad + fo.Wr, 1};
