@@ -208,7 +208,8 @@ def forward_kernel_name(n, graph, n_graphs=None):
     blocks of <= 224 rows -> the fp16x2 dense kernels; one graph of 224 < N <= 512 -> the fp16x2 DL kernels;
     N > 512 on one shared graph -> the shared-graph kernels (fp16x2 Linears).  All issue f16/bf16 MFMAs."""
     if n <= 224:
-        return "mpnn_forward_dense2_kernel"
+        return ("mpnn_forward_dense2_kernel" if int(os.environ.get("ECO_BENCH_KERNEL_PATHS", "0") or 0) & 16
+                else "mpnn_forward_dense3_kernel")
     if n <= 512:
         return "mpnn_forward_dl_kernel"
     return "shared_agg_kernel+shared_lin_kernel" if n_graphs == 1 else "mpnn_forward_large_kernel"
@@ -223,7 +224,7 @@ def mfma_roofline(achieved_tflops, kernel):
             "frac": achieved_tflops / peak, "peak_dtype": "f16/bf16 dense MFMA (the issued dtype)",
             "frac_vs_f32_mfma_peak": achieved_tflops / FP32_MFMA_PEAK_TFLOPS}
 # kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
-FWD_NAMES = ("mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
+FWD_NAMES = ("mpnn_forward_dense3_kernel", "mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
 BWD_NAMES = ("mpnn_backward_dense2_kernel", "mpnn_backward_dense_kernel")
 WGRAD_NAMES = ("wgrad_fh_kernel", "wgrad_bf3_kernel", "wgrad_kernel")
 
@@ -336,22 +337,28 @@ def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234, store=None):
     return B / (ms * 1e-3), ms
 
 
-def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000):
+def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000, graph="ER", gparam=0.15):
     """What the timed vector steps never contain (T = 2N steps per episode, 20 timed steps): the full reset of
     all B episodes at an episode boundary (fresh spins, compact-replay snapshot; dqn.py:306-327), and one
     evaluate_agent() at the reference's ER-200 test settings (train_eco.py:59-69,166-169,368-377: 50 test graphs,
     BEST metric, every 50k env-steps).  Both measured here with HIP-synchronised wall time and amortised per
-    vector step: reset / T, evaluation x (B x world / test_frequency)."""
+    vector step: reset / T, evaluation x (B / test_frequency).  The reset includes regenerating B fresh graphs
+    (regenerate_graphs, the reference's new graph per episode) on slots no transition references.  Evaluations:
+    learn() runs each crossing's evaluation on ONE rank (round-robin), so the per-rank cost per vector step is
+    evaluation x (B x world / test_frequency) / world = evaluation x B / test_frequency at any world size."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.agents.dqn.utils import TestMetric
     env, T, n = agent.env, agent.env.max_steps, agent.N
+    regen = agent.regenerate_graphs is not None and agent.graphs.n_graphs >= 2 * B
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if regen:  # slots [B, 2B): the next batch's, not referenced by any stored transition yet
+        agent.graphs.generate(B, B, graph, gparam, seed=agent.seed + 98, check=False)
     agent._reset_env(np.arange(B) % agent.graphs.n_graphs, agent.seed + 99)
     torch.cuda.synchronize()
     reset_ms = (time.perf_counter() - t0) * 1e3
-    test = VecSpinSystem(GraphStore.random("ER", test_graphs, n, 0.15, seed=4321, device=dev), 64, T,
+    test = VecSpinSystem(GraphStore.random(graph, test_graphs, n, gparam, seed=4321, device=dev), 64, T,
                          **env.env_args)
     saved = (agent.test_envs, agent.test_episodes, agent.test_metric)
     agent.test_envs, agent.test_episodes, agent.test_metric = test, test_graphs, TestMetric.BEST
@@ -378,15 +385,18 @@ def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000):
         ts.append((time.perf_counter() - t0) * 1e3)
     ov_ms = max(0.0, (ts[1] + ts[3] - ts[0] - ts[2]) / 2)
     agent.test_envs, agent.test_episodes, agent.test_metric = saved
-    per_vec_sync = reset_ms / T + eval_ms * (B * world / test_frequency)
-    per_vec = reset_ms / T + ov_ms * (B * world / test_frequency)
-    return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T,
+    per_vec_sync = reset_ms / T + eval_ms * (B / test_frequency)
+    per_vec = reset_ms / T + ov_ms * (B / test_frequency)
+    return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T, "reset_regenerates_graphs": regen,
             "evaluate_agent_ms": eval_ms, "evaluate_overlapped_ms": ov_ms,
             "evaluate_overlapped_note": f"wall time one overlapped evaluation adds to {k} vector steps of training "
                                         "(learn()'s default; evaluate_agent_ms is the synchronous call)",
             "evaluate_every_env_steps": test_frequency,
-            "evaluate_setting": f"{test_graphs} ER-{n} test graphs, BEST metric, {T} greedy steps each",
+            "evaluate_setting": f"{test_graphs} {graph}-{n} test graphs, BEST metric, {T} greedy steps each",
             "amortised_ms_per_vector_step": per_vec, "amortised_ms_per_vector_step_sync_eval": per_vec_sync,
+            "amortised_formula": "reset_ms / T + evaluate_overlapped_ms * (B * world / test_frequency) / world: one "
+                                 "evaluation per crossing for the whole job, dealt round-robin to the ranks "
+                                 "(DQN.learn), so the per-rank term is independent of world",
             "note": "not in the timed region: amortised, these would add this many ms to ms_per_step"}
 
 
@@ -490,7 +500,7 @@ def process_group_info(world, per_rank_s, steps, local, device):
 
 
 def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=1.0,
-                      n_graphs=None):
+                      n_graphs=None, regenerate=True):
     """The benched configs[2] / configs[3] agent: B episodes on a pool of B seeded graphs (one per episode),
     experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377) batched, with the large-batch recipe of
     tests/test_training_quality_gpu.py (target sync every update_target_frequency / update_frequency gradient
@@ -499,26 +509,35 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     (the reference's 15,000 transitions span ~19 whole ER-200 episodes); B x 16 (round 3) held only the last 16
     steps and measured 0.935 of the pretrained network's single-attempt cut against 0.974-0.991 with B x T
     (profiles/r04/quality/).  tests/test_training_quality_er200_gpu.py trains this exact agent.
-    n_graphs: size of the graph pool episodes draw from at each reset (default B).  Returns (agent, store, env, lr)."""
+    regenerate (default): a fresh ER / BA graph for every episode, as the reference's env.reset() draws one
+    (src/agents/dqn/dqn.py:306-327 -> src/envs/spinsystem.py:191-196 -> src/envs/utils.py:192-236): the store holds
+    graph_slots_needed(B, T, ring) slots (two batches of B at one episode's ring), generated on the device, and
+    DQN(regenerate_graphs=) regenerates a batch's slots at each reset once no stored transition references them.
+    regenerate=False: a fixed pool of n_graphs (default B) seeded graphs that episodes draw from at each reset.
+    Returns (agent, store, env, lr)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
                                     SpinBasis)
     from eco_hip.networks.mpnn import MPNN
-    from eco_hip.agents.dqn.dqn import DQN
+    from eco_hip.agents.dqn.dqn import DQN, graph_slots_needed
     T = 2 * n
-    store = GraphStore.random(graph, n_graphs or B, n, gparam, seed=seed, device=dev)
+    cap = int(B * T * replay_episodes)
+    if regenerate:
+        store = GraphStore.generated(graph, graph_slots_needed(B, T, cap), n, gparam, seed=seed, device=dev)
+    else:
+        store = GraphStore.random(graph, n_graphs or B, n, gparam, seed=seed, device=dev)
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
                         extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
                         spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
     lr = 1e-4 * (minibatch / 64.0) ** 0.5
-    cap = int(B * T * replay_episodes)
     agent = DQN(env, lambda: MPNN(device=dev), init_weight_std=0.01, double_dqn=True, clip_Q_targets=False,
                 replay_start_size=3000, replay_buffer_size=cap, gamma=0.95, update_target_frequency=4000,
                 update_learning_rate=False, initial_learning_rate=lr, peak_learning_rate=lr,
                 final_learning_rate=lr, update_frequency=32, minibatch_size=64, train_minibatch=minibatch,
                 initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
-                adam_epsilon=1e-8, seed=seed, target_sync="grad_steps")
+                adam_epsilon=1e-8, seed=seed, target_sync="grad_steps",
+                regenerate_graphs=(graph, gparam) if regenerate else None)
     return agent, store, env, lr
 
 
@@ -563,6 +582,9 @@ def main():
         torch.distributed.init_process_group(os.environ.get("ECO_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    if os.environ.get("ECO_BENCH_KERNEL_PATHS"):  # A/B knob (never set by the driver): eco_set_kernel_paths bits
+        from eco_hip import _lib
+        _lib.lib.eco_set_kernel_paths(int(os.environ["ECO_BENCH_KERNEL_PATHS"]))
 
     if args.workload in ("gset", "er20"):
         return inference_bench(args, world, rank, local, dev, dist)
@@ -609,7 +631,7 @@ def main():
     dt = max_over_ranks(dt_rank, device=dev)
     pg = process_group_info(world, dt_rank, args.steps, local, dev)
 
-    fixed = untimed_costs(agent, B, world, dev) if train else None
+    fixed = untimed_costs(agent, B, world, dev, graph=args.graph, gparam=gparam) if train else None
 
     # per-kernel roofline from the live events: forward launches vs backward launches
     kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}

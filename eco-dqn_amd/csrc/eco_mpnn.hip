@@ -51,6 +51,7 @@ __device__ unsigned long long eco_phase_ts[ECO_TS_BLOCKS * 32];
 }  // namespace eco
 #include "eco_mpnn_dense.h"  // dense-aggregation kernels (after the phase-timing buffer)
 #include "eco_mpnn_dense2.h"  // their fp16x2 successors
+#include "eco_mpnn_dense3.h"  // the fp16x2 forward, two tiles per wave
 #include "eco_mpnn_dl.h"      // one graph of 224 < N <= 512 per workgroup
 #include "eco_mpnn_shared.h"  // many episodes on one shared large graph (G22)
 namespace eco {
@@ -1116,7 +1117,8 @@ static std::atomic<int> g_kernel_paths{0};
 int eco::kernel_paths() { return g_kernel_paths.load(std::memory_order_relaxed); }
 
 extern "C" int32_t eco_set_kernel_paths(int32_t mask) {
-  return g_kernel_paths.exchange(mask & (ECO_PATH_NO_DENSE | ECO_PATH_NO_DL | ECO_PATH_NO_SHARED | ECO_PATH_NO_PAIR));
+  return g_kernel_paths.exchange(mask & (ECO_PATH_NO_DENSE | ECO_PATH_NO_DL | ECO_PATH_NO_SHARED | ECO_PATH_NO_PAIR |
+                                         ECO_PATH_DENSE2_FWD | 0xFF00));  // 0xFF00: kernel A/B variants
 }
 
 struct KCfg {
@@ -1212,7 +1214,8 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
   b.actions = actions_b;
   if (norm_scope == ECO_NORM_PER_CALL && !reuse_maxdeg)
     call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
-  return mpnn_forward_dense2_pair_launch(a, b, st);
+  if (paths & ECO_PATH_DENSE2_FWD) return mpnn_forward_dense2_pair_launch(a, b, st);
+  return mpnn_forward_dense3_pair_launch(a, b, st, paths >> 8);
 }
 
 extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
@@ -1241,7 +1244,8 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   }
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
-    return mpnn_forward_dense2_launch(a, saved != nullptr, st);
+    if (paths & ECO_PATH_DENSE2_FWD) return mpnn_forward_dense2_launch(a, saved != nullptr, st);
+    return mpnn_forward_dense3_launch(a, saved != nullptr, st, paths >> 8);
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_forward_dl_launch(a, saved != nullptr, workspace, st);
@@ -1324,4 +1328,88 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   else return fail(ECO_ERR_ARG, "graph block too large");
 #undef ECO_LAUNCH_BWD
   return check_launch("mpnn_backward");
+}
+
+// ---- split2_pk hazard probe (the v_fma_mix inline asm carries its own wait states) ----
+namespace eco {
+// One wave per 64 x 32 block of activations: the lane's four float4 split by split2_pk (inline asm) and fed to
+// MFMAs exactly as mm_fh feeds them (order 0) or with the lo fragment consumed first, straight after the asm (order
+// 1, the schedule most exposed to a missing wait state); the same products from the plain-conversion split
+// (split2_ref).  out[2][block][4 x 16 outputs][64 lanes] fp32 accumulators, compared bitwise by the test.
+template <bool REF>
+__device__ __forceinline__ void probe_split_fh(const float4& a, const float4& b, float sf, f16x8& hi, f16x8& lo) {
+  uint32_t h[4], l[4];
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (REF) split2_ref(v[2 * t], v[2 * t + 1], sf, h[t], l[t]);
+    else split2_pk(v[2 * t], v[2 * t + 1], sf, h[t], l[t]);
+  }
+  const u32x4v hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+  hi = __builtin_bit_cast(f16x8, hv);
+  lo = __builtin_bit_cast(f16x8, lv);
+}
+template <bool REF, int ORDER>
+__device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], float sf, const uint16_t* WH,
+                                         int lane) {
+  const uint16_t* wl = WH + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 xh, xl;
+    probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const f16x8 w1 = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      const f16x8 w2 = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      if (ORDER == 0) {  // mm_fh
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
+      } else {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
+      }
+    }
+  }
+}
+template <int ORDER>
+__global__ __launch_bounds__(256) void split2_probe_kernel(const float* x, const float* sf, const uint16_t* W,
+                                                           float* out, int n_blocks) {
+  __shared__ __attribute__((aligned(16))) uint16_t sWH[FH_HALF];
+  for (int i = threadIdx.x; i < FH_HALF / 8; i += 256)
+    reinterpret_cast<uint4*>(sWH)[i] = reinterpret_cast<const uint4*>(W)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk >= n_blocks) return;  // whole waves
+  float4 xv[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) xv[c] = f4(x + ((size_t)blk * 64 + lane) * 16 + 4 * c);
+  const float s = sf[blk];
+  f32x4 a[4], r[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) a[nt] = r[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  probe_mm<false, ORDER>(a, xv, s, sWH, lane);
+  probe_mm<true, ORDER>(r, xv, s, sWH, lane);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[(((size_t)0 * n_blocks + blk) * 16 + nt * 4 + i) * 64 + lane] = a[nt][i];
+      out[(((size_t)1 * n_blocks + blk) * 16 + nt * 4 + i) * 64 + lane] = r[nt][i];
+    }
+}
+}  // namespace eco
+
+extern "C" int eco_probe_split2_mfma(const float* x, const float* sf, const uint16_t* w_frags, int32_t n_blocks,
+                                     int32_t order, float* out, eco_stream_t stream) {
+  using namespace eco;
+  if (!x || !sf || !w_frags || !out || n_blocks < 1 || (order != 0 && order != 1))
+    return fail(ECO_ERR_ARG, "eco_probe_split2_mfma: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = (n_blocks + 3) / 4;
+  if (order == 0) split2_probe_kernel<0><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
+  else split2_probe_kernel<1><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
+  return check_launch("split2_probe");
 }

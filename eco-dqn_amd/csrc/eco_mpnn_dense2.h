@@ -74,8 +74,19 @@ __device__ __forceinline__ void split2_pk(float a, float b, float sf, uint32_t& 
   // the trailing s_nop: the hazard recognizer does not see inside inline asm, and an MFMA reading a VGPR written
   // by VALU needs 2 wait states (without it the fragments fed to the MFMAs were stale in some schedules)
   asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(sf), "v"(hi));
+#ifndef ECO_SPLIT2_NEGATIVE_CONTROL
   asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1" : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
+#else  // tests/test_split2_hazard_gpu.py's negative control (a tools build only): the wait states removed
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
+#endif
   lo = l;
+}
+// the same split by plain conversions (v_cvt_pk_f16_f32, f32 subtract, convert): the reference of
+// eco_probe_split2_mfma (bitwise equal to split2_pk by construction: a sf - hi is exact in f32)
+__device__ __forceinline__ void split2_ref(float a, float b, float sf, uint32_t& hi, uint32_t& lo) {
+  hi = pk_f16(a * sf, b * sf);
+  const f16x2v h = __builtin_bit_cast(f16x2v, hi);
+  lo = pk_f16(a * sf - (float)h[0], b * sf - (float)h[1]);
 }
 // 2^k as a float (k clamped to the normal range)
 __device__ __forceinline__ float exp2i(int k) {

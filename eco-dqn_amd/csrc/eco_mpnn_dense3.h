@@ -1,0 +1,703 @@
+// Dense-aggregation MPNN forward (src/networks/mpnn.py:40-159) on the fp16x2 operands of eco_mpnn_dense2.h, laid
+// out for TWO 16-node tiles per wave: 8 waves (2 per SIMD, 256 VGPRs each) per block of whole graphs, wave w owning
+// tiles 2w and 2w + 1 (h and e of both in registers).
+//
+// Why (round-5 ISA and SQ counters of the 16-wave dense2 kernel): with one tile per wave and the
+// 128-VGPR budget of 16 waves, every aggregation MFMA waited on a plane fragment read issued one MFMA earlier
+// (lgkmcnt(2) after each pair of ds_read_b64_tr_b16) and every Linear MFMA group on a weight fragment read issued
+// right before it (lgkmcnt(0)): the LDS latency was exposed on each 16-cycle MFMA, and 13 waves re-read the same
+// plane and weight fragments.  Here each fragment read feeds the MFMAs of both tiles (half the LDS traffic per MFMA),
+// the two tiles' chains interleave (no dependent back-to-back MFMAs), and the 256-VGPR budget keeps a whole chunk's
+// plane fragments and a whole Linear half's weight fragments in flight.
+//
+// Numerics are those of mpnn_forward_dense2_kernel operation by operation: every accumulator receives the same
+// MFMAs with the same operands in the same order (tile pairs whose chunk ranges differ -- several graphs per block --
+// run the union range; the extra chunks carry all-zero adjacency fragments and add +-0 to a sum that starts at +0),
+// the same scales, splits and f32 epilogues, so the two kernels are bitwise equal
+// (tests/test_dense_gpu.py::test_dense3_matches_dense2_bitwise).  Saved activations, masks and the readout are
+// written in dense2's layout (the backward is shared).
+#pragma once
+#include "eco_mpnn_dense2.h"
+
+namespace eco {
+
+constexpr int D3_NW = 8;  // waves per workgroup
+// aggregation of the wave's two tiles: the pipelined straight-line form when every chunk is live (VAR bit 0)
+#define AGG3(M, acc, P0, P1, adjw, sc, kc0, kc1, lane)                                        \
+  do {                                                                                      \
+    if ((VAR & 1) && kc0 == 0 && kc1 == DN_KC) agg3f<M>(acc, P0, P1, adjw, sc, lane);       \
+    else agg3<M>(acc, P0, P1, adjw, sc, kc0, kc1, lane);                                    \
+  } while (0)
+
+// acc[t][ft] += sum over chunks kc in [kc0, kc1) and both planes of Hs[j][16ft + ..] . B_t[j][node] for the wave's
+// two tiles t = 0, 1 (products h 2^c); each plane fragment read feeds both tiles' MFMAs.  adjw[t][kc]: spread
+// adjacency words of tile t; sc: agg_scale of the planes.  EXEC all ones (wave-uniform branches only).
+template <int MODE>
+__device__ __forceinline__ void agg3(f32x4 (&acc)[2][4], const uint16_t* P0, const uint16_t* P1,
+                                     const uint32_t (&adjw)[2][DN_KC], const AggScale& sc, int kc0, int kc1,
+                                     int lane) {
+  const int q = lane >> 4;
+  const int j_in = 4 * q + ((lane >> 2) & 3);
+  const int pc = (lane & 3) ^ q;
+#pragma unroll
+  for (int kc = 0; kc < DN_KC; ++kc) {
+    if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
+    const uint32_t plo = __builtin_amdgcn_readlane(sc.pat, 2 * kc);
+    const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
+    const f16x8 b0 = adj_frag2<MODE>(adjw[0][kc], plo, phi);
+    const f16x8 b1 = adj_frag2<MODE>(adjw[1][kc], plo, phi);
+    const int off = (32 * kc + j_in) * 16 + 4 * pc;
+    f16x8 af[2][4];
+#pragma unroll
+    for (int p = 1; p >= 0; --p) {
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        const uint16_t* a = (p ? P1 : P0) + off + ft * (DN_KPMAX * 16);
+        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
+        const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[p][ft] = __builtin_bit_cast(f16x8, raw);
+      }
+    }
+#pragma unroll
+    for (int p = 1; p >= 0; --p) {  // the small plane first (dense2's order per accumulator)
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        acc[0][ft] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[p][ft], b0, acc[0][ft], 0, 0, 0);
+        acc[1][ft] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[p][ft], b1, acc[1][ft], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// agg3 software-pipelined for blocks whose every wave runs chunks 0 .. DN_KC - 1 (one graph of 193 .. 224 rows:
+// ER-200): straight-line code, chunk kc + 1's 16 plane reads and adjacency fragments issued into the other register
+// set while chunk kc's 16 MFMAs run, interleaved one MFMA / one read / two VALU by sched_group_barrier (the
+// compiler's own schedule waited on every pair of fragments: lgkmcnt(0) before each group of four MFMAs).  Same
+// MFMAs per accumulator in the same order as agg3.
+template <int MODE>
+__device__ __forceinline__ void agg3f(f32x4 (&acc)[2][4], const uint16_t* P0, const uint16_t* P1,
+                                      const uint32_t (&adjw)[2][DN_KC], const AggScale& sc, int lane) {
+  const int q = lane >> 4;
+  const int j_in = 4 * q + ((lane >> 2) & 3);
+  const int pc = (lane & 3) ^ q;
+  f16x8 fa[2][8], fb[2][2];
+  auto issue = [&](int kc, int buf) {
+    const int off = (32 * kc + j_in) * 16 + 4 * pc;
+#pragma unroll
+    for (int p = 1; p >= 0; --p) {
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        const uint16_t* a = (p ? P1 : P0) + off + ft * (DN_KPMAX * 16);
+        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
+        const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[buf][(1 - p) * 4 + ft] = __builtin_bit_cast(f16x8, raw);
+      }
+    }
+    const uint32_t plo = __builtin_amdgcn_readlane(sc.pat, 2 * kc);
+    const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
+    fb[buf][0] = adj_frag2<MODE>(adjw[0][kc], plo, phi);
+    fb[buf][1] = adj_frag2<MODE>(adjw[1][kc], plo, phi);
+  };
+  issue(0, 0);
+#pragma unroll
+  for (int kc = 0; kc < DN_KC; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < DN_KC) issue(kc + 1, cur ^ 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // i = (1 - p) * 4 + ft: the small plane first
+      acc[0][i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[cur][i], fb[cur][0], acc[0][i & 3], 0, 0, 0);
+      acc[1][i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[cur][i], fb[cur][1], acc[1][i & 3], 0, 0, 0);
+    }
+    if (kc + 1 < DN_KC) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // chunk kc + 1's reads stay in this group (ahead of their MFMAs)
+  }
+}
+
+// acc[t][nt] += W[16nt + .][one 64-input half] . x_t for both tiles, x_t = hi + lo (split_fh with the tile's node
+// scale sf[t]); every weight fragment read feeds both tiles.  Per accumulator the products of mm_fh in its order.
+__device__ __forceinline__ void mm_fh_2t(f32x4 (&acc)[2][4], const float4 (&x0)[4], const float4 (&x1)[4],
+                                         const float (&sf)[2], const uint16_t* WH, int lane) {
+  const uint16_t* wl = WH + lane * 8;
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 wf1[4], wf2[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      wf1[nt] = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      wf2[nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+    }
+    f16x8 xh0, xl0, xh1, xl1;
+    split_fh(x0[2 * kc2], x0[2 * kc2 + 1], sf[0], xh0, xl0);
+    split_fh(x1[2 * kc2], x1[2 * kc2 + 1], sf[1], xh1, xl1);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf2[nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf2[nt], xh1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xl0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xl1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xh1, acc[1][nt], 0, 0, 0);
+    }
+  }
+}
+
+// A whole 128-input Linear for both tiles, as mm_fh_2t(x_a, W_a) then mm_fh_2t(x_b, W_b) (the same products per
+// accumulator in the same order), software-pipelined over its four 32-input steps: step s + 1's eight weight
+// fragments are read while step s's inputs are split and its 24 MFMAs run (sched_barrier keeps each step's reads
+// ahead of their MFMAs instead of right before them).
+__device__ __forceinline__ void lin128_2t(f32x4 (&acc)[2][4], const float4 (&xa0)[4], const float4 (&xa1)[4],
+                                          const uint16_t* WA, const float4 (&xb0)[4], const float4 (&xb1)[4],
+                                          const uint16_t* WB, const float (&sf)[2], int lane) {
+  f16x8 w1[2][4], w2[2][4];
+  auto issue = [&](int s, int buf) {
+    const uint16_t* wl = (s < 2 ? WA : WB) + lane * 8;
+    const int kc2 = s & 1;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      w1[buf][nt] = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      w2[buf][nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+    }
+  };
+  issue(0, 0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < 4) issue(s + 1, cur ^ 1);
+    const int kc2 = s & 1;
+    f16x8 xh0, xl0, xh1, xl1;
+    if (s < 2) {
+      split_fh(xa0[2 * kc2], xa0[2 * kc2 + 1], sf[0], xh0, xl0);
+      split_fh(xa1[2 * kc2], xa1[2 * kc2 + 1], sf[1], xh1, xl1);
+    } else {
+      split_fh(xb0[2 * kc2], xb0[2 * kc2 + 1], sf[0], xh0, xl0);
+      split_fh(xb1[2 * kc2], xb1[2 * kc2 + 1], sf[1], xh1, xl1);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[cur][nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[cur][nt], xh1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xl0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xl1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xh1, acc[1][nt], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void zero_acc2(f32x4 (&d)[2][4]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) d[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Staging of the wave's two tiles (d2_stage per tile): row norms, max degrees and spread adjacency words.  One
+// graph per block with a prepared gs.adjbits: per-lane loads; otherwise row info / edge bases / max degrees in LDS
+// and the block bitmask built once (barriers: uniform over the workgroup).
+template <int NT>
+__device__ __forceinline__ void d3_stage(const MpnnArgs& a, int blk, int rows_pad, int rows_valid, const int (&r)[2],
+                                         const bool (&valid)[2], int s4, int2* RI, int64_t* GB, int* MD,
+                                         uint32_t* ADJ, float (&nf)[2], int (&md)[2],
+                                         uint32_t (&adjw)[2][DN_KC]) {
+  const int N = a.N;
+  uint32_t adjb[2][4];
+  if (a.gpb == 1 && a.gs.adjbits != nullptr) {
+    const int gid = a.gids[blk];  // uniform: scalar load
+    const int mdg = a.gs.max_deg[gid];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int dg = valid[t] ? a.gs.deg[(size_t)gid * N + r[t]] : 1;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (valid[t]) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + r[t]) * 4 + s4) * 4);
+      adjb[t][0] = v.x; adjb[t][1] = v.y; adjb[t][2] = v.z; adjb[t][3] = v.w;
+      nf[t] = (float)max(dg, 1);
+      md[t] = mdg;
+    }
+  } else {
+    const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+    for (int r2 = threadIdx.x; r2 < rows_pad; r2 += NT) RI[r2] = pack_row_info(a, blk, r2, rows_valid);
+    for (int gl = threadIdx.x; gl < g_valid; gl += NT) {
+      const int gid = a.gids[blk * a.gpb + gl];
+      GB[gl] = a.gs.edge_base[gid];
+      MD[gl] = a.gs.max_deg[gid];
+    }
+    lds_barrier();
+    const bool built = adj_build<NT>(a, ADJ, RI, GB, rows_pad, rows_valid);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int rr = min(r[t], rows_pad - 1);
+      nf[t] = (float)row_info(RI, rr).norm;
+      md[t] = valid[t] ? MD[r[t] / N] : 1;
+      adj_lane(a, ADJ, built, blk, r[t], rr, valid[t], s4, adjb[t]);
+    }
+    if (built) __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kc = 0; kc < DN_KC; ++kc) adjw[t][kc] = adj_spread((adjb[t][kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+}
+
+// LDS (ECO_D2_LDS), as mpnn_forward_dense2_kernel.  NNET = 2: the online and the target network on the same graphs
+// and features (a0 then a1), sharing the staging.
+template <bool SAVE, int NNET, int VAR>
+__global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(MpnnArgs a0, MpnnArgs a1) {
+  ECO_D2_LDS;
+  const MpnnArgs& a = a0;  // the staging reads the graph fields, equal in a0 and a1
+  ECO_TS(0);
+  constexpr int NW = D3_NW;
+  constexpr int NT = 64 * NW;
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  uint16_t* PL = sPL;
+  uint16_t* PL1 = sPL + D2_PLANE;
+  uint16_t* WB0 = sW0;
+  uint16_t* WB1 = sW1;
+  uint16_t* WB2 = sW2;
+  int* TE = sTE;
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(sPL);  // [rows_pad][DN_ADJW] while a bitmask is built
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+
+  const bool act = 2 * w < ntiles;  // the wave computes both of its tiles (a padding tile on zeros)
+  int tl[2], r[2];
+  bool has[2], valid[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    tl[t] = 2 * w + t;
+    has[t] = tl[t] < ntiles;
+    r[t] = tl[t] * 16 + c16;
+    valid[t] = has[t] && r[t] < rows_valid;
+  }
+  // ---- staging: Wf fragments (LDS-DMA); node features, the 8-input Linears' weights and w_a; row norms, max
+  //      degrees and adjacency operands of the lane's two rows ----
+  glds_frags<NW>(WB0, PH + FH_WF, 16, w, lane);
+  float xk0[2], xk1[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    xk0[t] = 0.f;
+    xk1[t] = 0.f;
+    if (valid[t]) {
+      xk0[t] = a.x[(R0 + r[t]) * 8 + s4];
+      xk1[t] = a.x[(R0 + r[t]) * 8 + 4 + s4];
+    }
+  }
+  float wx8[8], w08[8];
+  lin8_load(P + PK_WX, lane, wx8);
+  lin8_load(P + PK_W0, lane, w08);
+  float4 wa4[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
+  float nf[2];
+  int md_graph[2];
+  uint32_t adjw[2][DN_KC];
+  d3_stage<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, sRI, sGB, sMD, ADJ, nf, md_graph, adjw);
+  ECO_TS(1);
+  float rnf[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
+  // aggregation chunks of the wave's rows (the union of its two tiles' ranges)
+  const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  // one network (a: its weights and outputs); next: the network that runs after it in this launch, or null.
+  // Called once per network with its own argument struct (no per-field selects between a0 and a1).
+  auto net_body = [&](const MpnnArgs& a, const MpnnArgs* next, bool first) __attribute__((always_inline)) {
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  int kw[FH_NMAT];  // the matrix scales, wave-uniform
+#pragma unroll
+  for (int m = 0; m < FH_NMAT; ++m) kw[m] = __builtin_amdgcn_readfirstlane(fh_kw(P, m));
+  if (!first) {
+    lin8_load(P + PK_WX, lane, wx8);
+    lin8_load(P + PK_W0, lane, w08);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
+  }
+  zero_pad_rows2<NT>(PL, PL1, rows_pad);
+  zero_pad_rows2<NT>(WB1, WB2, rows_pad);  // V planes
+
+  // ---- phase A: Z = Wx . x (f32 MFMA); U = relu(Z + w_a) and V = relu(Z - w_a) planes ----
+  if (act) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 z[4];
+      lin8r(z, wx8, xk0[t], xk1[t]);
+      float4 u[4], v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 wa = wa4[c];
+        u[c] = valid[t] ? make_float4(relu(fmaf(1.f, wa.x, z[c][0])), relu(fmaf(1.f, wa.y, z[c][1])),
+                                      relu(fmaf(1.f, wa.z, z[c][2])), relu(fmaf(1.f, wa.w, z[c][3])))
+                        : zero4();
+        v[c] = valid[t] ? make_float4(relu(fmaf(-1.f, wa.x, z[c][0])), relu(fmaf(-1.f, wa.y, z[c][1])),
+                                      relu(fmaf(-1.f, wa.z, z[c][2])), relu(fmaf(-1.f, wa.w, z[c][3])))
+                        : zero4();
+      }
+      if (has[t]) {
+        tile_planes(PL, PL1, TE, tl[t], r[t], s4, u, lane);
+        tile_planes(WB1, WB2, TE + 16, tl[t], r[t], s4, v, lane);
+      }
+    }
+  }
+  glds_wait();  // Wf fragments
+  lds_barrier();
+  ECO_TS(2);
+
+  // ---- phase B: edge embedding (mpnn.py:89-104): (A+ . relu(Z + w_a) + A- . relu(Z - w_a)) / norm; Wf ----
+  float4 ereg[2][4];
+  {
+    const AggScale su = agg_scale(TE, ntiles, lane);
+    const AggScale sv = agg_scale(TE + 16, ntiles, lane);
+    f32x4 ea[2][4], ev[2][4];
+    zero_acc2(ea);
+    zero_acc2(ev);
+    if (act) {
+      AGG3(1, ea, PL, PL1, adjw, su, kc0, kc1, lane);
+      AGG3(2, ev, WB1, WB2, adjw, sv, kc0, kc1, lane);
+    }
+    const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
+    float4 acc[2][4];
+    float sfx[2];
+    int kx[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float t4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          t4[i] = (__builtin_ldexpf(ea[t][c][i], -su.c) + __builtin_ldexpf(ev[t][c][i], -sv.c)) * rnf[t];
+        acc[t][c] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+      }
+      // feature 63 = norm / norm.max()  (mpnn.py:102)
+      const int md = a.norm_scope == ECO_NORM_PER_CALL ? maxdeg_call : (valid[t] ? md_graph[t] : 1);
+      if (s4 == 3) acc[t][3].w = nf[t] / (float)md;
+      if (!valid[t]) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[t][c] = zero4();
+      } else if (SAVE) {
+        float* eap = a.sv + (size_t)SV_EAGG * RT * 64 + (R0 + r[t]) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st4(eap + 16 * c, acc[t][c]);
+      }
+      kx[t] = node_exp<4>(acc[t]);
+      sfx[t] = exp2i(kx[t]);
+    }
+    f32x4 d[2][4];
+    zero_acc2(d);
+    if (act) mm_fh_2t(d, acc[0], acc[1], sfx, WB0, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      unscale(d[t], kx[t] + kw[0]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        ereg[t][nt] = relu4(d[t][nt]);
+        if (SAVE && valid[t])
+          st4(a.sv + (size_t)SV_E * RT * 64 + (R0 + r[t]) * 64 + 16 * nt + 4 * s4, ereg[t][nt]);
+      }
+      if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_E, pos_mask(ereg[t]));
+    }
+  }
+  lds_barrier();  // every wave is done with the U / V planes and with Wf
+  ECO_TS(3);
+  // layer weights: Wm0 -> WB1, Wu0 -> WB2, Wm1 -> WB0 (landed by layer 0's first barrier)
+  glds_frags<NW>(WB1, PH + FH_LAYER, 32, w, lane);
+  glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_HALF, 32, w, lane);
+  glds_frags<NW>(WB0, PH + FH_LAYER + FH_LAYER_STRIDE, 32, w, lane);
+
+  // ---- phase C: h0 = relu(W0 . x) (mpnn.py:20-23, :55), in registers + planes ----
+  float4 hreg[2][4];
+  if (act) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 z[4];
+      lin8r(z, w08, xk0[t], xk1[t]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        hreg[t][c] = valid[t] ? relu4(z[c]) : zero4();
+        if (SAVE && valid[t])
+          st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r[t]) * 64 + 16 * c + 4 * s4, hreg[t][c]);
+      }
+      if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
+      if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_H0, pos_mask(hreg[t]));
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) hreg[t][c] = zero4();
+  }
+  lds_barrier();
+  ECO_TS(4);
+
+  // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
+  for (int layer = 0; layer < 3; ++layer) {
+    const uint16_t* WM = layer == 0 ? WB1 : (layer == 1 ? WB0 : WB2);
+    const uint16_t* WU = layer == 0 ? WB2 : (layer == 1 ? WB1 : WB0);
+    if (layer == 1) {
+      glds_frags<NW>(WB1, PH + FH_LAYER + FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu1
+      glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_LAYER_STRIDE, 32, w, lane);            // Wm2
+    } else if (layer == 2) {
+      glds_frags<NW>(WB0, PH + FH_LAYER + 2 * FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu2
+    }
+    const AggScale sh = agg_scale(TE, ntiles, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[t][kc]));  // no hoisting of the fragment masks
+    f32x4 ag[2][4];
+    zero_acc2(ag);
+    if (act) AGG3(0, ag, PL, PL1, adjw, sh, kc0, kc1, lane);
+    float4 agg[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float sc = __builtin_ldexpf(rnf[t], -sh.c);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        agg[t][c] = make_float4(ag[t][c][0] * sc, ag[t][c][1] * sc, ag[t][c][2] * sc, ag[t][c][3] * sc);
+    }
+    glds_wait();
+    lds_barrier();  // B1: planes read by every wave; this layer's weights landed
+    if (layer == 0) ECO_TS(11);
+    if (SAVE) {  // after the wait: stores count in vmcnt with the weight DMA
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (!valid[t]) continue;
+        float* sa = a.sv + (size_t)(SV_AGG0 + layer) * RT * 64 + (R0 + r[t]) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st4(sa + 16 * c, agg[t][c]);
+      }
+    }
+    // message = relu(Wm . [agg, e])
+    float4 mrel[2][4];
+    {
+      f32x4 d[2][4];
+      zero_acc2(d);
+      int kx[2];
+      float sf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kx[t] = node_exp2(agg[t], ereg[t]);
+        sf[t] = exp2i(kx[t]);
+      }
+      if (act) {
+        if constexpr (VAR & 2) {
+          lin128_2t(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
+        } else {
+          mm_fh_2t(d, ereg[0], ereg[1], sf, WM + FH_HALF, lane);
+          mm_fh_2t(d, agg[0], agg[1], sf, WM, lane);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        unscale(d[t], kx[t] + kw[1 + 2 * layer]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) mrel[t][c] = relu4(d[t][c]);
+      }
+    }
+    if (SAVE) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (!valid[t]) continue;
+        float* sm = a.sv + (size_t)(SV_M0 + layer) * RT * 64 + (R0 + r[t]) * 64 + 4 * s4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st4(sm + 16 * c, mrel[t][c]);
+        store_mask(a, RT, R0 + r[t], s4, SM_M0 + layer, pos_mask(mrel[t]));
+      }
+    }
+    if (layer == 0) ECO_TS(12);
+    // h' = relu(Wu . [h, m])
+    {
+      f32x4 hn[2][4];
+      zero_acc2(hn);
+      int kx[2];
+      float sf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kx[t] = node_exp2(hreg[t], mrel[t]);
+        sf[t] = exp2i(kx[t]);
+      }
+      if (act) {
+        if constexpr (VAR & 2) {
+          lin128_2t(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
+        } else {
+          mm_fh_2t(hn, hreg[0], hreg[1], sf, WU, lane);
+          mm_fh_2t(hn, mrel[0], mrel[1], sf, WU + FH_HALF, lane);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        unscale(hn[t], kx[t] + kw[2 + 2 * layer]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          hreg[t][c] = valid[t] ? relu4(hn[t][c]) : zero4();
+          if (SAVE && valid[t])
+            st4(a.sv + (size_t)(SV_H0 + layer + 1) * RT * 64 + (R0 + r[t]) * 64 + 16 * c + 4 * s4, hreg[t][c]);
+        }
+        if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_H1 + layer, pos_mask(hreg[t]));
+      }
+    }
+    if (layer == 0) ECO_TS(13);
+    if (layer < 2) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
+    }
+    lds_barrier();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
+    ECO_TS(5 + layer);
+  }
+  if (next)  // the next network's Wf into the free buffer, landing while this readout runs
+    glds_frags<NW>(WB0, reinterpret_cast<const uint16_t*>(next->P + PK_FH) + FH_WF, 16, w, lane);
+
+  // ---- phase E: readout (mpnn.py:143-159) + act ----
+  if (a.gpb == 1) {
+    // one graph: per node q_local = Wr[64:] . h3 and per tile the column sums of h3 go to LDS from registers; one
+    // barrier; wave 0 reduces the tile partials in tile order, forms p = Wp . mean, relu(p) . Wr[:64], q and acts
+    float* COL = reinterpret_cast<float*>(sPL);  // [ntiles][64]
+    float* QL = COL + 16 * 64;                    // [rows_pad] q_local
+    float* MEANS = QL + DN_MAX_ROWS;              // [64]
+    float* QB = MEANS + 64;                       // [rows_pad] q
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (!has[t]) continue;
+      float ql = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 wr = f4(P + PK_WR + 64 + 16 * c + 4 * s4);
+        ql = fmaf(hreg[t][c].x, wr.x, ql);
+        ql = fmaf(hreg[t][c].y, wr.y, ql);
+        ql = fmaf(hreg[t][c].z, wr.z, ql);
+        ql = fmaf(hreg[t][c].w, wr.w, ql);
+      }
+      auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(ql), __float_as_uint(ql), false, false);
+      ql = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+      auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ql), __float_as_uint(ql), false, false);
+      ql = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+      if (s4 == 0) QL[r[t]] = ql;
+      float cs[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        cs[4 * c] = row_sum16(hreg[t][c].x);
+        cs[4 * c + 1] = row_sum16(hreg[t][c].y);
+        cs[4 * c + 2] = row_sum16(hreg[t][c].z);
+        cs[4 * c + 3] = row_sum16(hreg[t][c].w);
+      }
+      if (c16 == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          st4(COL + tl[t] * 64 + 16 * c + 4 * s4, make_float4(cs[4 * c], cs[4 * c + 1], cs[4 * c + 2], cs[4 * c + 3]));
+      }
+    }
+    lds_barrier();
+    if (w == 0) {
+      float cs = 0.f;
+      for (int t = 0; t < ntiles; ++t) cs += COL[t * 64 + lane];  // tile order
+      const float mean = cs / (float)N;
+      MEANS[lane] = mean;
+      wave_lds_sync();
+      const float* wp = P + PK_WP + lane * 64;
+      float p = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float4 wv = f4(wp + 4 * k), mv = f4(MEANS + 4 * k);
+        p = fmaf(wv.x, mv.x, p);
+        p = fmaf(wv.y, mv.y, p);
+        p = fmaf(wv.z, mv.z, p);
+        p = fmaf(wv.w, mv.w, p);
+      }
+      if (SAVE) {
+        a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)blk * 64 + lane] = mean;
+        a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)a.B * 64 + (size_t)blk * 64 + lane] = p;
+      }
+      const float cg = wave_sum_f(relu(p) * P[PK_WR + lane]);
+      const float br = P[PK_BR];
+      for (int i = lane; i < N; i += 64) {
+        const float qv = cg + QL[i] + br;
+        QB[i] = qv;
+        if (a.q) a.q[R0 + i] = qv;
+      }
+      if (a.has_act) {
+        wave_lds_sync();
+        graph_act<NW>(a, QB, blk, 1, R0);
+      }
+    }
+    ECO_TS(8);
+    if (next) lds_barrier();  // wave 0's readout scratch (the plane array) before the next planes
+    return;
+  }
+  // several graphs per block: h3 rows staged as fp32 [rows][D2_HS_LD] in the plane array
+  float* Hs = reinterpret_cast<float*>(sPL);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (!has[t]) continue;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st4(Hs + r[t] * D2_HS_LD + 16 * c + 4 * s4, hreg[t][c]);
+  }
+  lds_barrier();
+  float* Scr = reinterpret_cast<float*>(sW1);
+  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= D2_WBUF_BYTES;
+  if (!split && readout_scratch_floats(rows_pad, a.gpb, NW, false) * 4 > D2_WBUF_BYTES) return;  // launch checks
+  readout_act<SAVE, NW>(a, Hs, D2_HS_LD, Scr, split, blk, g_valid, rows_valid, R0, RT);
+  ECO_TS(8);
+  if (next) lds_barrier();
+  };  // net_body
+  net_body(a0, NNET == 2 ? &a1 : nullptr, true);
+  if constexpr (NNET == 2) net_body(a1, nullptr, false);
+}
+
+static int dense3_check(const MpnnArgs& a) {
+  const int rows_pad = (a.gpb * a.N + 15) & ~15;
+  if (rows_pad > DN_MAX_ROWS || a.gpb > D2_MAX_GPB) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS tables");
+  if (readout_scratch_floats(rows_pad, a.gpb, D3_NW, false) * 4 > D2_WBUF_BYTES)
+    return fail(ECO_ERR_ARG, "dense MPNN readout scratch exceeds its buffer");
+  return ECO_OK;
+}
+
+template <int VAR>
+static int mpnn_forward_dense3_launch_v(const MpnnArgs& a, bool save, hipStream_t st) {
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  if (save) mpnn_forward_dense3_kernel<true, 1, VAR><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  else mpnn_forward_dense3_kernel<false, 1, VAR><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  return check_launch("mpnn_forward_dense3");
+}
+static int mpnn_forward_dense3_launch(const MpnnArgs& a, bool save, hipStream_t st, int var) {
+  if (const int rc = dense3_check(a)) return rc;
+  switch (var & 3) {
+    case 1: return mpnn_forward_dense3_launch_v<1>(a, save, st);
+    case 2: return mpnn_forward_dense3_launch_v<2>(a, save, st);
+    case 3: return mpnn_forward_dense3_launch_v<3>(a, save, st);
+    default: return mpnn_forward_dense3_launch_v<0>(a, save, st);
+  }
+}
+static int mpnn_forward_dense3_pair_launch(const MpnnArgs& a, const MpnnArgs& b, hipStream_t st, int var) {
+  if (const int rc = dense3_check(a)) return rc;
+  if (a.gpb != 1) return fail(ECO_ERR_ARG, "paired dense forward: one graph per block only");
+  switch (var & 3) {
+    case 1: mpnn_forward_dense3_kernel<false, 2, 1><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
+    case 2: mpnn_forward_dense3_kernel<false, 2, 2><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
+    case 3: mpnn_forward_dense3_kernel<false, 2, 3><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
+    default: mpnn_forward_dense3_kernel<false, 2, 0><<<a.B, 64 * D3_NW, 0, st>>>(a, b);
+  }
+  return check_launch("mpnn_forward_dense3_pair");
+}
+
+}  // namespace eco

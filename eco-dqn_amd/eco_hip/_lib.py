@@ -33,7 +33,7 @@ ECO_COMPACT_MAX_SPINS = 8192  # include/eco_hip.h: compact replay (sample rebuil
 ECO_NORM_PER_GRAPH, ECO_NORM_PER_CALL, ECO_NORM_PER_CALL_REUSE = 0, 1, 2
 ECO_GRAPH_ER, ECO_GRAPH_BA = 1, 2
 # kernel-path policy bits (eco_set_kernel_paths)
-ECO_PATH_NO_DENSE, ECO_PATH_NO_DL, ECO_PATH_NO_SHARED, ECO_PATH_NO_PAIR = 1, 2, 4, 8
+ECO_PATH_NO_DENSE, ECO_PATH_NO_DL, ECO_PATH_NO_SHARED, ECO_PATH_NO_PAIR, ECO_PATH_DENSE2_FWD = 1, 2, 4, 8, 16
 
 
 class EnvConfig(ctypes.Structure):
@@ -82,6 +82,7 @@ _SIG = {
     "eco_env_read": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P, _P, _P]),
     "eco_check_errors": (ctypes.c_int, [_P]),
     "eco_set_kernel_paths": (_I, [_I]),
+    "eco_probe_split2_mfma": (ctypes.c_int, [_P, _P, _P, _I, _I, _P, _P]),
     "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), ctypes.POINTER(GraphSet), _P, _I, _P,
                                               _P]),
     "eco_mpnn_param_count": (ctypes.c_size_t, [_I]),

@@ -102,6 +102,14 @@ class DQN:
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
         self.world = torch.distributed.get_world_size() if self.dist else 1
         broadcast_parameters(self.network.flat)  # every rank starts from rank 0's weights
+        # evaluations use rank 0's seed on every rank (learn() runs each evaluation of the job on one rank: its
+        # episodes' initial spins must not depend on which rank that is); = seed in one process
+        self.eval_seed = self.seed
+        if self.dist and self.world > 1:
+            t = torch.tensor([self.seed], dtype=torch.int64,
+                             device=self.device if torch.distributed.get_backend() == "nccl" else "cpu")
+            torch.distributed.broadcast(t, src=0)
+            self.eval_seed = int(t.item())
         self.target_network.load_state_dict(self.network.state_dict())
         n = self.network.flat.numel()
         self.grad = torch.zeros(n, dtype=torch.float32, device=self.device)
@@ -447,12 +455,24 @@ class DQN:
         (:349-364); every `save_network_frequency` env-steps save `<network_save_path><t>` (:366-372);
         at the end pickle test_scores / losses / solutions (:377-394).  A vector step that crosses
         k * frequency counts as reaching timestep k * frequency.  Files are written by rank 0.
+
+        Multi-GPU: each crossing is ONE evaluation of the job, run by one rank (evaluation e by rank e mod world,
+        on its test env: the same episodes and test graphs as a single-process evaluation at that timestep); its
+        scores reach every rank through a small all-reduce at a fixed point (when evaluation e + world starts, or
+        at the end of learn()), so the evaluation work per rank per vector step does not grow with the world
+        size.  Rank 0 keeps a copy of the weights of every evaluation in flight for `_best` (the parameters are
+        bit-identical across ranks).
         Returns the last 100 (timestep, loss) pairs."""
         import pickle
+        from collections import deque
         self.start()
         rank = torch.distributed.get_rank() if self.dist else 0
+        world = self.world
         test_scores, test_solutions = [], []
-        pending = None  # an overlapped evaluation in flight
+        inflight = deque()   # evaluations launched, not yet recorded (index order)
+        n_eval = 0           # evaluations launched by the job so far (every rank counts the same)
+        test_env0 = self._test_env() if self.evaluate else None
+        cursor0 = getattr(test_env0, "_eval_next_graph", 0) if test_env0 is not None else 0
 
         def record(tk, test_score, test_solution, net):
             if verbose and rank == 0:
@@ -464,8 +484,39 @@ class DQN:
             test_scores.append([tk, test_score])
             test_solutions.append([tk, test_solution])
 
-        def finish(p):
-            record(p["tk"], *self._eval_one_fill_finish(p), p["net"])
+        def collect(e):
+            """Record evaluation e on every rank (the same call order everywhere: the all-reduce is collective)."""
+            if e["owner"] == rank:
+                sc, so = self._eval_one_fill_finish(e["p"]) if "p" in e else e["result"]
+            else:
+                sc, so = 0.0, 0.0
+            if world > 1:
+                t = torch.tensor([sc, so], dtype=torch.float64,
+                                 device=self.device if torch.distributed.get_backend() == "nccl" else "cpu")
+                torch.distributed.all_reduce(t)  # only the owner contributes: the sum is its result
+                sc, so = float(t[0]), float(t[1])
+            record(e["tk"], sc, so, e["net"])
+
+        def launch(tk):
+            nonlocal n_eval
+            owner = n_eval % world
+            e = {"tk": tk, "owner": owner, "idx": n_eval, "net": None}
+            n_eval += 1
+            if owner == rank:
+                env = self._test_env()
+                n_graphs = env.graphs.n_graphs
+                env._eval_next_graph = (cursor0 + e["idx"] * self.test_episodes) % n_graphs  # job-wide order
+                if self._overlap_ok(env):
+                    e["p"] = self._evaluate_overlapped(tk)
+                    e["net"] = e["p"]["net"]
+                else:
+                    e["result"] = self.evaluate_agent()
+                    e["net"] = self.network
+            if rank == 0 and owner != rank:  # the weights at tk, for _best
+                snap = self._network_factory()
+                snap.flat.copy_(self.network.flat)
+                e["net"] = snap
+            inflight.append(e)
 
         while self._timestep < timesteps:
             t_prev = self._timestep
@@ -480,24 +531,19 @@ class DQN:
                 # graphs regenerated with check=False since the last sync point: an edge-slot overflow
                 # sets the device error word (the slot becomes an empty graph); surface it here
                 self.graphs.check_errors()
-            if pending is not None and pending["done"].query():
-                finish(pending)
-                pending = None
+            if world == 1 and inflight and "p" in inflight[0] and inflight[0]["p"]["done"].query():
+                collect(inflight.popleft())  # finished early (one process: no collective to keep in step)
             if self.evaluate and crossed_test:
                 tk = (t // self.test_frequency) * self.test_frequency
-                if pending is not None:  # one evaluation in flight at a time (its snapshot is reused)
-                    finish(pending)
-                    pending = None
-                if self.overlap_evaluation and self._one_fill_ok(self._test_env(), None):
-                    pending = self._evaluate_overlapped(tk)
-                else:
-                    record(tk, *self.evaluate_agent(), self.network)
+                while len(inflight) >= world:  # this evaluation's owner runs one evaluation at a time
+                    collect(inflight.popleft())
+                launch(tk)
             if t // self.save_network_frequency > t_prev // self.save_network_frequency and rank == 0:
                 tk = (t // self.save_network_frequency) * self.save_network_frequency
                 main, ext = os.path.splitext(self.network_save_path)
                 self.save(main + str(tk) + (ext or ".pth"))
-        if pending is not None:
-            finish(pending)
+        while inflight:
+            collect(inflight.popleft())
         if self.regenerate_graphs is not None:
             self.graphs.check_errors()
         losses = self.losses()
@@ -513,7 +559,19 @@ class DQN:
                 if verbose:
                     print('saved to {}'.format(p_))
         self.test_scores, self.test_solutions = test_scores, test_solutions
+        self.evaluations_run = sum(1 for i in range(n_eval) if i % world == rank)  # by this rank
         return losses[-100:]
+
+    def _overlap_ok(self, env):
+        """learn() overlaps an evaluation with training (side stream, weight snapshot) when it takes the one-fill
+        path, the test env runs on the default stream (its kernels are then ordered by the side stream alone), and
+        training cannot rewrite the test env's graphs meanwhile (regenerate_graphs on the store the test env reads,
+        i.e. test_envs=None): otherwise the evaluation runs synchronously."""
+        if not (self.overlap_evaluation and self._one_fill_ok(env, None)):
+            return False
+        if getattr(env, "stream", None) is not None:
+            return False
+        return not (self.regenerate_graphs is not None and env.graphs is self.graphs)
 
     def losses(self):
         """[[timestep, loss], ...] of every gradient step of the current (or last) learn() call
@@ -551,7 +609,7 @@ class DQN:
             env._eval_next_graph = 0
         n_graphs = env.graphs.n_graphs
         # every slot holds a valid episode (unused ones run to their end and stay masked)
-        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.seed)
+        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.eval_seed)
         active = torch.zeros(env.n_envs, dtype=torch.bool, device=dev)
         cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
         acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
@@ -567,7 +625,7 @@ class DQN:
                 gids = np.zeros(env.n_envs, dtype=np.int64)
                 gids[take] = (env._eval_next_graph + np.arange(len(take))) % n_graphs
                 env._eval_next_graph = (env._eval_next_graph + len(take)) % n_graphs
-                env.reset(graph_ids=gids, mask=mask, seed=self.seed + started)
+                env.reset(graph_ids=gids, mask=mask, seed=self.eval_seed + started)
                 active[torch.as_tensor(take, device=dev)] = True
                 cum[torch.as_tensor(take, device=dev)] = 0.0
                 started += len(take)
@@ -635,13 +693,13 @@ class DQN:
         if not hasattr(env, "_eval_next_graph"):
             env._eval_next_graph = 0
         # every slot holds a valid episode (unused ones run to their end and stay masked), as evaluate_agent
-        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.seed)
+        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.eval_seed)
         mask = np.zeros(env.n_envs, dtype=np.uint8)
         mask[:k] = 1
         gids = np.zeros(env.n_envs, dtype=np.int64)
         gids[:k] = (env._eval_next_graph + np.arange(k)) % n_graphs
         env._eval_next_graph = (env._eval_next_graph + k) % n_graphs
-        env.reset(graph_ids=gids, mask=mask, seed=self.seed)
+        env.reset(graph_ids=gids, mask=mask, seed=self.eval_seed)
         cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
         acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
         sub = acts[:k]

@@ -233,5 +233,10 @@ class SingleGraphGenerator(SetGraphGenerator):
     """One known graph (src/envs/utils.py:319-345): every get() returns it (with its bias, when given)."""
 
     def __init__(self, matrix, bias=None):
-        super().__init__([matrix], None if bias is None else [bias], ordered=True)
+        # the reference's single-graph generator checks no bias length (src/envs/utils.py:319-345), so the set
+        # generator's n_spins + 1 assertion is not applied here: the pair is stored as given
+        super().__init__([matrix], None, ordered=True)
         self.matrix, self.bias = matrix, bias
+        if bias is not None:
+            self.biased = True
+            self.graphs = [(matrix, bias)]

@@ -246,10 +246,21 @@ int eco_mpnn_forward_pair(const float *packed_a, const float *packed_b, int32_t 
  *   NO_DENSE  -- blocks the dense-aggregation kernels would take run the CSR-gather kernels instead;
  *   NO_DL     -- one-graph blocks of 224 < N <= 512 run the CSR-gather kernels;
  *   NO_SHARED -- N > 512 single-graph inference runs the per-episode global-memory kernel;
- *   NO_PAIR   -- eco_mpnn_forward_pair runs as two eco_mpnn_forward calls.
+ *   NO_PAIR   -- eco_mpnn_forward_pair runs as two eco_mpnn_forward calls;
+ *   DENSE2_FWD -- dense-aggregation forwards (N <= 224 blocks) run the one-tile-per-wave 16-wave kernel instead of
+ *                 the two-tiles-per-wave 8-wave one (bitwise the same results; A/B and cross-check).
  * The library reads no environment variables; this call is the only switch. Returns the previous mask. */
-enum { ECO_PATH_NO_DENSE = 1, ECO_PATH_NO_DL = 2, ECO_PATH_NO_SHARED = 4, ECO_PATH_NO_PAIR = 8 };
+enum { ECO_PATH_NO_DENSE = 1, ECO_PATH_NO_DL = 2, ECO_PATH_NO_SHARED = 4, ECO_PATH_NO_PAIR = 8, ECO_PATH_DENSE2_FWD = 16 };
 int32_t eco_set_kernel_paths(int32_t mask);
+
+/* Test probe of the fp16x2 operand split (no reference counterpart; guards the dense kernels' inline-asm
+ * v_fma_mix split, which carries its own MFMA wait states -- src/networks/mpnn.py:111-118 is the Linear it feeds).
+ * n_blocks blocks of 64 nodes x 16 fp32 activations x[n_blocks][64][16], per-block power-of-two scale sf[n_blocks],
+ * one 64-input half of fp16x2 weight fragments w_frags (16 fragments of 512 fp16, the PK_FH layout); order 0 feeds
+ * the MFMAs as the dense kernels do, order 1 consumes the lo piece first.  out[2][n_blocks][16][64]: the fp32
+ * accumulators from the asm split, then from a plain-conversion split -- bitwise equal when the split is sound. */
+int eco_probe_split2_mfma(const float *x, const float *sf, const uint16_t *w_frags, int32_t n_blocks, int32_t order,
+                          float *out, eco_stream_t stream);
 
 /* ---- DQN train step (dqn.py:403-451) ---- */
 

@@ -1,0 +1,86 @@
+"""One rank of tests/test_parallel_gpu.py::test_two_ranks_evaluate_once_per_crossing (not a test module):
+DQN.learn() with evaluations over gloo, both ranks on GPU 0.  B x world = 256 env-steps per vector step against
+test_frequency = 200, so EVERY vector step crosses a test point (the regime of configs[3] at 8 GPUs).  Each
+crossing must be one evaluation of the job (owner = evaluation index mod world), every rank must record the same
+test scores, and the `_best` checkpoint rank 0 writes must reproduce the best recorded score when evaluated again.
+Rank 0 prints EVAL_OK <evaluations> <per-rank counts> <best score>."""
+import os
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "eco-dqn_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN
+    from eco_hip.agents.dqn.utils import TestMetric
+    n, B = 20, 128
+    kw = dict(observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS, extra_action=ExtraAction.NONE,
+              optimisation_target=OptimisationTarget.CUT, spin_basis=SpinBasis.SIGNED, norm_rewards=True,
+              basin_reward=1. / n)
+    store = GraphStore.random("ER", 512, n, 0.15, seed=60 + rank, device="cuda:0")
+    env = VecSpinSystem(store, B, 2 * n, **kw)
+    # the same test graphs on every rank (train_eco.py's fixed test set)
+    test = VecSpinSystem(GraphStore.random("ER", 10, n, 0.15, seed=777, device="cuda:0"), 16, 2 * n, **kw)
+    tmp = tempfile.mkdtemp(prefix=f"eco_eval_r{rank}_")
+    agent = DQN(env, lambda: MPNN(device="cuda:0"), init_weight_std=0.01, double_dqn=True, replay_start_size=2 * B,
+                replay_buffer_size=4096, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
+                initial_learning_rate=1e-3, peak_learning_rate=1e-3, final_learning_rate=1e-3, update_frequency=32,
+                minibatch_size=16, train_minibatch=128, final_exploration_rate=0.05, final_exploration_step=20000,
+                seed=21 + rank, evaluate=True, test_envs=test, test_episodes=10, test_frequency=200,
+                test_metric=TestMetric.BEST, test_save_path=os.path.join(tmp, "scores"),
+                network_save_path=os.path.join(tmp, "net.pth"), save_network_frequency=10 ** 9)
+    timesteps = B * world * 2 * n * 2
+    agent.learn(timesteps=timesteps)
+    # crossings of the timed loop: every vector step once training is ready
+    ts = np.array([t for t, _ in agent.test_scores])
+    sc = torch.tensor([s for _, s in agent.test_scores], dtype=torch.float64)
+    allsc = [torch.zeros_like(sc) for _ in range(world)]
+    dist.all_gather(allsc, sc)
+    runs = torch.tensor([float(agent.evaluations_run)])
+    allruns = [torch.zeros_like(runs) for _ in range(world)]
+    dist.all_gather(allruns, runs)
+    # constructed on every rank (the constructor's parameter / seed broadcasts are collective)
+    chk = DQN(env, lambda: MPNN(device="cuda:0"), init_weight_std=0.01, replay_start_size=2 * B,
+              replay_buffer_size=4096, minibatch_size=16, seed=21 + rank, evaluate=False, test_envs=test,
+              test_episodes=10, test_metric=TestMetric.BEST, test_save_path=None)
+    if rank == 0:
+        assert all(torch.equal(a, allsc[0]) for a in allsc), "ranks recorded different test scores"
+        assert len(ts) == len(np.unique(ts)) and np.all(np.diff(ts) > 0)
+        per_vec = B * world
+        first_ready = ts[0]
+        expect = [t for t in range(first_ready, timesteps + 1, 200)]
+        # one evaluation per vector step that crosses k * 200 (every step here): count the crossed steps
+        steps = np.arange(per_vec, timesteps + 1, per_vec)
+        crossed = [t for t in steps if t // 200 > (t - per_vec) // 200 and t >= first_ready]
+        assert len(ts) == len(crossed), (len(ts), len(crossed), len(expect))
+        counts = [int(r.item()) for r in allruns]
+        assert sum(counts) == len(ts) and max(counts) - min(counts) <= 1, counts
+        # the _best checkpoint reproduces the best score (evaluation seed = rank 0's on every rank)
+        best = float(sc.max())
+        chk.load(os.path.join(tmp, "net_best.pth"))
+        i_best = int(np.argmax(sc.numpy()))  # first occurrence = the evaluation that saved _best
+        test._eval_next_graph = (i_best * 10) % 10
+        again, _ = chk.evaluate_agent()
+        assert again == best, (again, best)
+        print("EVAL_OK", len(ts), counts, best, flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -221,3 +221,62 @@ def test_norm_per_call_reuse(n, B, p):
     net.forward_graphs(xc[: sub.numel()].contiguous(), store, sub, norm_scope=ECO_NORM_PER_CALL)
     q_again = net.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL)
     assert torch.equal(q_ref, q_again)
+
+
+@pytest.mark.parametrize("n,B,p,prepared", [(200, 300, 0.15, True), (224, 9, 0.15, True), (150, 16, 0.3, True),
+                                            (200, 10, 0.15, False), (20, 4101, 0.15, False), (64, 19, 0.2, False),
+                                            (104, 33, 0.1, False)])
+def test_dense3_matches_dense2_bitwise(n, B, p, prepared):
+    """The two-tiles-per-wave forward (eco_mpnn_dense3.h, 8 waves) against the one-tile-per-wave forward
+    (eco_mpnn_dense2.h, 16 waves, ECO_PATH_DENSE2_FWD): the same MFMAs per accumulator in the same order, so Q,
+    the fused epsilon-greedy actions, every saved activation and ReLU mask, the backward's gradients and the paired
+    s' forward are bitwise equal -- one graph per block (prepared bitmask or built in-kernel, 13 / 14 tiles, a padded
+    last tile) and several graphs per block (ER-20 x 4101: 10-graph blocks and a 1-graph tail)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip import _lib
+    from eco_hip._lib import ActConfig, ECO_NORM_PER_CALL, ECO_NORM_PER_GRAPH
+    store = GraphStore.random("ER", B, n, p, seed=n + B)
+    if not prepared:
+        store.gs.adjbits = None
+    g = torch.Generator().manual_seed(3 * n + B)
+    na, nb = MPNN(device="cuda"), MPNN(device="cuda")
+    na.load_state_dict(mo.init_weights(g, std=0.1))
+    nb.load_state_dict(mo.init_weights(g, std=0.1))
+    x = torch.zeros(B, n, 8)
+    x[:, :, :7] = torch.rand(B, n, 7, generator=g) * 2 - 1
+    x[:, :, 0] = torch.where(x[:, :, 0] > 0, 1.0, -1.0)
+    xc = x.cuda()
+    gids = torch.randperm(B, generator=g).to(torch.int32).cuda()
+    dq = torch.randn(B, n, generator=g).cuda()
+
+    def run(mask):
+        with _lib.kernel_paths(mask):
+            out = {}
+            acts = torch.empty(B, dtype=torch.int32, device="cuda")
+            out["q"] = na.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_GRAPH,
+                                         act=ActConfig(0.3, 1, 0.0, 11, 5), actions_out=acts,
+                                         q_out=torch.empty(B, n, device="cuda")).clone()
+            out["acts"] = acts.clone()
+            saved = torch.zeros(MPNN.saved_bytes(n, B), dtype=torch.uint8, device="cuda")
+            out["qs"] = na.forward_graphs(xc, store, gids, norm_scope=ECO_NORM_PER_CALL, saved=saved).clone()
+            out["saved"] = saved
+            grad = torch.zeros_like(na.flat)
+            na.backward_graphs(xc, store, gids, saved, dq, grad)
+            out["grad"] = grad
+            a_star = torch.empty(B, dtype=torch.int32, device="cuda")
+            qa, qb = torch.empty(B, n, device="cuda"), torch.empty(B, n, device="cuda")
+            na.forward_pair_graphs(nb, xc, store, gids, norm_scope=ECO_NORM_PER_CALL, q_out=qa,
+                                   act=ActConfig(0.0, 1, 0.0, 0, 0), actions_out=a_star, q_out_other=qb)
+            out["pair"] = (qa, qb, a_star)
+            torch.cuda.synchronize()
+            return out
+
+    old = run(_lib.ECO_PATH_DENSE2_FWD)
+    for variant in (0, 1 << 8, 2 << 8, 3 << 8):  # the default and the kernel's A/B schedules (bits 8-9)
+        new = run(variant)
+        assert torch.isfinite(new["q"]).all()
+        for k in ("q", "acts", "qs", "saved", "grad"):
+            assert torch.equal(new[k], old[k]), (variant, k)
+        for u, v in zip(new["pair"], old["pair"]):
+            assert torch.equal(u, v), variant

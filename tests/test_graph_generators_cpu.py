@@ -46,3 +46,16 @@ def test_mixed_dimensions_rejected():
     from eco_hip.envs.utils import SetGraphGenerator
     with pytest.raises(NotImplementedError):
         SetGraphGenerator([np.zeros((4, 4)), np.zeros((5, 5))])
+
+
+def test_single_graph_generator_takes_any_bias_length():
+    """The reference's SingleGraphGenerator stores (matrix, bias) as given (src/envs/utils.py:319-345): an N-long bias
+    is accepted (the set generator's N + 1 check does not apply) and returned with the matrix on every get()."""
+    from eco_hip.envs.utils import SingleGraphGenerator
+    J = _graphs(np.random.default_rng(3), 9, 1, "discrete")[0]
+    bias = np.arange(9, dtype=float)
+    gen = SingleGraphGenerator(J, bias)
+    assert gen.biased
+    for _ in range(3):
+        m, b = gen.get()
+        assert m is J and b is bias

@@ -22,13 +22,13 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_two_ranks_train_to_identical_parameters():
-    world, port = 2, str(_port())
+def _run_ranks(worker, world=2):
+    port = str(_port())
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port, HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_train_worker.py")], env=env,
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, worker)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     for p in procs:
@@ -40,6 +40,12 @@ def test_two_ranks_train_to_identical_parameters():
             raise
         outs.append(out)
         assert p.returncode == 0, out[-3000:]
+    return outs
+
+
+def test_two_ranks_train_to_identical_parameters():
+    world = 2
+    outs = _run_ranks("dist_train_worker.py", world)
     ex = next(l for l in outs[0].splitlines() if l.startswith("EXCHANGE_OK")).split()
     assert int(ex[1]) == 3 and float(ex[2]) < 1e-5
     line = next(l for l in outs[0].splitlines() if l.startswith("DIST_OK"))
@@ -50,3 +56,13 @@ def test_two_ranks_train_to_identical_parameters():
     assert diff == 0.0           # identical updates on every rank
     assert moved > 0.0
     assert "True" in parts[5] and parts[5].count(str(steps)) >= world
+
+
+def test_two_ranks_evaluate_once_per_crossing():
+    """learn() with evaluations at two ranks, every vector step crossing a test point (B x world > test_frequency,
+    configs[3]'s regime at 8 GPUs): exactly one evaluation per crossing for the job, dealt round-robin to the ranks,
+    the same test scores recorded on every rank, and the `_best` checkpoint reproducing the best score
+    (dist_eval_worker.py)."""
+    outs = _run_ranks("dist_eval_worker.py", 2)
+    line = next(l for l in outs[0].splitlines() if l.startswith("EVAL_OK"))
+    assert int(line.split()[1]) > 4
