@@ -1306,7 +1306,8 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   a.gr = (float*)gradws;
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
-    return mpnn_backward_dense2_launch(a, st);
+    if (paths & ECO_PATH_DENSE2_FWD) return mpnn_backward_dense2_launch(a, st);
+    return mpnn_backward_dense3_launch(a, st, paths >> 8);
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_backward_dl_launch(a, st);

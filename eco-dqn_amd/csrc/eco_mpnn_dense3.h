@@ -700,4 +700,433 @@ static int mpnn_forward_dense3_pair_launch(const MpnnArgs& a, const MpnnArgs& b,
   return check_launch("mpnn_forward_dense3_pair");
 }
 
+
+// ============================================================== backward ====
+// Two output halves (fragment sets WH0, WH1) of one 64-input transposed Linear for both tiles, sharing each tile's
+// split of x and every weight fragment read (mm_fh2's products per accumulator, in its order).
+__device__ __forceinline__ void mm_fh2_2t(f32x4 (&acc0)[2][4], f32x4 (&acc1)[2][4], const float4 (&x0)[4],
+                                          const float4 (&x1)[4], const float (&sf)[2], const uint16_t* WH0,
+                                          const uint16_t* WH1, int lane) {
+#pragma unroll
+  for (int kc2 = 0; kc2 < 2; ++kc2) {
+    f16x8 xh0, xl0, xh1, xl1;
+    split_fh(x0[2 * kc2], x0[2 * kc2 + 1], sf[0], xh0, xl0);
+    split_fh(x1[2 * kc2], x1[2 * kc2 + 1], sf[1], xh1, xl1);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint16_t* wl = (hh ? WH1 : WH0) + lane * 8;
+      f16x8 wf1[4], wf2[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        wf1[nt] = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+        wf2[nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4& a0 = hh ? acc1[0][nt] : acc0[0][nt];
+        f32x4& a1 = hh ? acc1[1][nt] : acc0[1][nt];
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf2[nt], xh0, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf2[nt], xh1, a1, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xl0, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xl1, a1, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xh0, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf1[nt], xh1, a1, 0, 0, 0);
+      }
+    }
+  }
+}
+
+// Autograd of the forward (dqn.py:440-449): mpnn_backward_dense2_kernel's operations, laid out as the forward here
+// (8 waves, tiles 2w and 2w + 1 per wave, shared fragment reads).  Every sum keeps dense2's order -- the readout's
+// strided node sums run over 16 virtual waves, dw_a's per-tile partials are summed in tile order over 16 slots --
+// so the gradients are bitwise those of mpnn_backward_dense2_kernel (tests/test_dense_gpu.py).
+// LDS (ECO_D2_LDS): sPL 2 planes (readout scratch first) | sW0, sW1, sW2 | TE | RI | GB
+template <int VAR>
+__global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(MpnnArgs a) {
+  ECO_D2_LDS;
+  ECO_TS(16);
+  constexpr int NW = D3_NW;
+  constexpr int NT = 64 * NW;
+  constexpr int VNW = 16;  // dense2's wave count: the order of the readout's strided sums and of dw_a
+  const int lane = threadIdx.x & 63;
+  const int w = uniform_i(threadIdx.x >> 6);
+  const int blk = blockIdx.x;
+  const int N = a.N;
+  const int g_valid = min(a.gpb, a.B - blk * a.gpb);
+  const int rows_valid = g_valid * N;
+  const int rows_pad = (a.gpb * N + 15) & ~15;
+  const int ntiles = rows_pad >> 4;
+  uint16_t* PL = sPL;
+  uint16_t* PL1 = sPL + D2_PLANE;
+  uint32_t* ADJ = reinterpret_cast<uint32_t*>(sPL);
+  float* lds = reinterpret_cast<float*>(sPL);  // readout / dw_a scratch
+  uint16_t* WB0 = sW0;
+  uint16_t* WB1 = sW1;
+  uint16_t* WB2 = sW2;
+  int* TE = sTE;
+  const size_t R0 = (size_t)blk * a.gpb * N;
+  const size_t RT = (size_t)a.B * N;
+  const float* P = a.P;
+  const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
+  const float* sv = a.sv;
+  float* gr = a.gr;
+  const int s4 = lane >> 4;
+  const int c16 = lane & 15;
+  auto SV = [&](int t) { return sv + (size_t)t * RT * 64; };
+  auto GR = [&](int t) { return gr + (size_t)t * RT * 64; };
+  const float* MEAN = sv + (size_t)SV_NODE_TENSORS * RT * 64;
+  const float* PP = MEAN + (size_t)a.B * 64;
+  float* DP = gr + (size_t)GR_NODE_TENSORS * RT * 64;
+  float* DWRA = DP + (size_t)a.B * 64;
+  float* DWRB = DWRA + (size_t)a.B * 64;
+  float* DBR = DWRB + (size_t)a.B * 64;
+  float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
+  auto WUT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE + 2 * FH_HALF; };  // Wu^T: 2 output halves
+  auto WMT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE; };                // Wm^T: dagg, de halves
+  int kw[FH_NMAT];
+#pragma unroll
+  for (int m = 0; m < FH_NMAT; ++m) kw[m] = __builtin_amdgcn_readfirstlane(fh_kw(P, m));
+
+  // ---- staging: Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (LDS-DMA), row info, edge bases ----
+  glds_frags<NW>(WB0, WUT(2), 32, w, lane);
+  glds_frags<NW>(WB1, WMT(2), 32, w, lane);
+  glds_frags<NW>(WB2, WUT(1), 32, w, lane);
+  const bool act = 2 * w < ntiles;
+  int tl[2], rw[2], rr[2];
+  bool has[2], valid[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    tl[t] = 2 * w + t;
+    has[t] = tl[t] < ntiles;
+    rw[t] = tl[t] * 16 + c16;
+    valid[t] = has[t] && rw[t] < rows_valid;
+    rr[t] = min(rw[t], rows_pad - 1);
+  }
+  float nf[2], rnf[2];
+  int md_unused[2];
+  uint32_t adjw[2][DN_KC];
+  d3_stage<NT>(a, blk, rows_pad, rows_valid, rw, valid, s4, sRI, sGB, sMD, ADJ, nf, md_unused, adjw);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
+  const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
+  const int kc0 = (g_lo * N) >> 5;
+  const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
+  const uint16_t* Msk = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
+  uint4 rmask[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    rmask[t] = valid[t] ? *reinterpret_cast<const uint4*>(Msk + ((R0 + rw[t]) * 4 + s4) * SM_TENSORS)
+                        : make_uint4(0u, 0u, 0u, 0u);
+  ECO_TS(17);
+
+  // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
+  float* DQ = lds;                       // [rows_pad]
+  float* DMEAN = DQ + rows_pad;          // [gpb][64]
+  float* RED = DMEAN + a.gpb * 64;       // [gpb][VNW][64] (split)
+  const bool split = a.gpb < VNW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * VNW * 64) * 4 <= (size_t)D2_PL_BYTES;
+  for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
+  lds_barrier();
+  if (split) {  // dWr[64:] = sum_v dq_v h3_v, over dense2's 16 strided partial sums (virtual waves w, w + 8)
+    for (int gl = 0; gl < g_valid; ++gl) {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int vw = w + NW * u;
+        float dwb = 0.f;
+        for (int v = vw; v < N; v += VNW) {
+          const float dv = DQ[gl * N + v];
+          if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+        }
+        RED[(gl * VNW + vw) * 64 + lane] = dwb;
+      }
+    }
+    lds_barrier();
+  }
+  for (int gl = w; gl < g_valid; gl += NW) {
+    const int e = blk * a.gpb + gl;
+    float sacc = 0.f;
+    for (int v = lane; v < N; v += 64) sacc += DQ[gl * N + v];
+    const float S = wave_sum_f(sacc);
+    const float p = PP[(size_t)e * 64 + lane];
+    const float dp = P[PK_WR + lane] * S * (p > 0.f ? 1.f : 0.f);
+    DP[(size_t)e * 64 + lane] = dp;
+    DWRA[(size_t)e * 64 + lane] = relu(p) * S;
+    if (lane == 0) DBR[e] = S;
+    float dmean = 0.f;
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k)
+      dmean = fmaf(P[PK_WP + k * 64 + lane], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dp), k)), dmean);
+    DMEAN[gl * 64 + lane] = dmean / (float)N;
+    float dwb = 0.f;
+    if (split) {
+#pragma unroll
+      for (int k = 0; k < VNW; ++k) dwb += RED[(gl * VNW + k) * 64 + lane];  // fixed order
+    } else {
+      const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
+      for (int v = 0; v < N; ++v) {
+        const float dv = DQ[gl * N + v];
+        if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
+      }
+    }
+    DWRB[(size_t)e * 64 + lane] = dwb;
+  }
+  lds_barrier();
+  // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
+  float4 dh[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float dqi = valid[t] ? DQ[rw[t]] : 0.f;
+    const int gl = rr[t] / N;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 16 * c + 4 * s4;
+      const float4 dm = valid[t] ? f4(DMEAN + gl * 64 + f) : zero4();
+      dh[t][c] = make_float4(fmaf(dqi, P[PK_WR + 64 + f + 0], dm.x), fmaf(dqi, P[PK_WR + 64 + f + 1], dm.y),
+                             fmaf(dqi, P[PK_WR + 64 + f + 2], dm.z), fmaf(dqi, P[PK_WR + 64 + f + 3], dm.w));
+    }
+  }
+  glds_wait();     // Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (staged at the start) are read from here on
+  lds_barrier();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
+  zero_pad_rows2<NT>(PL, PL1, rows_pad);
+  ECO_TS(18);
+
+  // ---- update layers in reverse (mpnn.py:114-120) ----
+  float4 de[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) de[t][c] = zero4();
+  for (int layer = 2; layer >= 0; --layer) {
+    const uint16_t* WU = layer == 2 ? WB0 : (layer == 1 ? WB2 : WB1);
+    const uint16_t* WM = layer == 2 ? WB1 : (layer == 1 ? WB0 : WB2);
+    // duu = dh' * [h' > 0]  (in place in dh)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t hmask = mask16(rmask[t], SM_H0 + layer + 1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        dh[t][c] = masked(f32x4{dh[t][c].x, dh[t][c].y, dh[t][c].z, dh[t][c].w}, hmask, c);
+    }
+    // [dh_direct, dm] = Wu^T . duu;  dum = dm * [m > 0]
+    f32x4 dhd[2][4];
+    float4 dum[2][4];
+    {
+      f32x4 dmm[2][4];
+      zero_acc2(dhd);
+      zero_acc2(dmm);
+      int kx[2];
+      float sf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kx[t] = node_exp<4>(dh[t]);
+        sf[t] = exp2i(kx[t]);
+      }
+      if (act) mm_fh2_2t(dhd, dmm, dh[0], dh[1], sf, WU, WU + FH_HALF, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ku = kx[t] + kw[2 + 2 * layer];
+        unscale(dhd[t], ku);
+        unscale(dmm[t], ku);
+        const uint32_t mmask = mask16(rmask[t], SM_M0 + layer);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dum[t][c] = masked(dmm[t][c], mmask, c);
+      }
+    }
+    if (layer == 1) ECO_TS(24);
+    glds_wait();
+    lds_barrier();  // B0: Wm^T landed
+    if (layer == 1) ECO_TS(25);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (!valid[t]) continue;  // stored after the wait: stores count in vmcnt with the weight DMA
+      const size_t ro = (R0 + rr[t]) * 64 + 4 * s4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        st4(GR(GR_DUU0 + layer) + ro + 16 * c, dh[t][c]);
+        st4(GR(GR_DUM0 + layer) + ro + 16 * c, dum[t][c]);
+      }
+    }
+    // [dagg, de] = Wm^T . dum;  G = dagg / norm -> planes
+    {
+      f32x4 dg[2][4], dd[2][4];
+      zero_acc2(dg);
+      zero_acc2(dd);
+      int kx[2];
+      float sf[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        kx[t] = node_exp<4>(dum[t]);
+        sf[t] = exp2i(kx[t]);
+      }
+      if (act) mm_fh2_2t(dg, dd, dum[0], dum[1], sf, WM, WM + FH_HALF, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int km = kx[t] + kw[1 + 2 * layer];
+        unscale(dg[t], km);
+        unscale(dd[t], km);
+        float4 g[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          de[t][c].x += dd[t][c][0]; de[t][c].y += dd[t][c][1]; de[t][c].z += dd[t][c][2]; de[t][c].w += dd[t][c][3];
+          g[c] = valid[t] ? make_float4(dg[t][c][0] * rnf[t], dg[t][c][1] * rnf[t], dg[t][c][2] * rnf[t],
+                                        dg[t][c][3] * rnf[t])
+                          : zero4();
+        }
+        if (has[t]) tile_planes(PL, PL1, TE, tl[t], rw[t], s4, g, lane);
+      }
+    }
+    if (layer == 1) ECO_TS(26);
+    lds_barrier();  // B1: G planes complete; every wave is past both Linears: this layer's weight buffers free
+    if (layer == 2) {
+      glds_frags<NW>(WB0, WMT(1), 32, w, lane);
+      glds_frags<NW>(WB1, WUT(0), 32, w, lane);
+    } else if (layer == 1) {
+      glds_frags<NW>(WB2, WMT(0), 32, w, lane);
+      glds_frags<NW>(WB0, PH + FHT_WF, 16, w, lane);  // Wf^T for the edge layer
+    }
+    if (layer == 1) ECO_TS(27);
+    // dh_layer = dh_direct + A^T . G  (A symmetric: the forward aggregation)
+    {
+      const AggScale sg = agg_scale(TE, ntiles, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[t][kc]));
+      f32x4 ag[2][4];
+      zero_acc2(ag);
+      if (act) AGG3(0, ag, PL, PL1, adjw, sg, kc0, kc1, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float t4[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) t4[i] = dhd[t][c][i] + __builtin_ldexpf(ag[t][c][i], -sg.c);
+          dh[t][c] = valid[t] ? make_float4(t4[0], t4[1], t4[2], t4[3]) : zero4();
+        }
+    }
+    if (layer == 1) ECO_TS(28);
+    lds_barrier();  // B2: planes read
+    ECO_TS(21 - layer);
+  }
+
+  // ---- h0 = relu(W0.x): du0;  edge embedding (mpnn.py:89-104): due, dEagg = Wf^T . due -> G planes ----
+  glds_wait();
+  lds_barrier();  // Wf^T landed
+  {
+    float4 due[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const size_t ro = (R0 + rr[t]) * 64 + 4 * s4;
+      const uint32_t h0m = mask16(rmask[t], SM_H0), em = mask16(rmask[t], SM_E);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (valid[t])
+          st4(GR(GR_DU0) + ro + 16 * c, masked(f32x4{dh[t][c].x, dh[t][c].y, dh[t][c].z, dh[t][c].w}, h0m, c));
+        due[t][c] = masked(f32x4{de[t][c].x, de[t][c].y, de[t][c].z, de[t][c].w}, em, c);
+        if (valid[t]) st4(GR(GR_DUE) + ro + 16 * c, due[t][c]);
+      }
+    }
+    f32x4 dg[2][4];
+    zero_acc2(dg);
+    int kx[2];
+    float sf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      kx[t] = node_exp<4>(due[t]);
+      sf[t] = exp2i(kx[t]);
+    }
+    if (act) mm_fh_2t(dg, due[0], due[1], sf, WB0, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      unscale(dg[t], kx[t] + kw[0]);
+      float4 g[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        g[c] = valid[t] ? make_float4(dg[t][c][0] * rnf[t], dg[t][c][1] * rnf[t], dg[t][c][2] * rnf[t],
+                                      dg[t][c][3] * rnf[t])
+                        : zero4();
+      if (has[t]) tile_planes(PL, PL1, TE, tl[t], rw[t], s4, g, lane);
+    }
+  }
+  lds_barrier();
+  ECO_TS(22);
+  // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
+  {
+    float xk0[2], xk1[2];  // inputs of Z, loaded ahead of the aggregations
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      xk0[t] = 0.f;
+      xk1[t] = 0.f;
+      if (valid[t]) {
+        xk0[t] = a.x[(R0 + rw[t]) * 8 + s4];
+        xk1[t] = a.x[(R0 + rw[t]) * 8 + 4 + s4];
+      }
+    }
+    float wx8[8];
+    lin8_load(P + PK_WX, lane, wx8);
+    float4 wa4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
+    const AggScale sg = agg_scale(TE, ntiles, lane);
+    f32x4 gp[2][4], gm[2][4];
+    zero_acc2(gp);
+    zero_acc2(gm);
+    if (act) {
+      AGG3(1, gp, PL, PL1, adjw, sg, kc0, kc1, lane);
+      AGG3(2, gm, PL, PL1, adjw, sg, kc0, kc1, lane);
+    }
+    float dwacc[2][16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 zz[4];
+      lin8r(zz, wx8, xk0[t], xk1[t]);  // Z exactly as the forward computed it
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float dz4[4];
+        const float wav[4] = {wa4[c].x, wa4[c].y, wa4[c].z, wa4[c].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float z = zz[c][i];
+          const float wa = wav[i];
+          const float tp = fmaf(1.f, wa, z) > 0.f ? __builtin_ldexpf(gp[t][c][i], -sg.c) : 0.f;
+          const float tm = fmaf(-1.f, wa, z) > 0.f ? __builtin_ldexpf(gm[t][c][i], -sg.c) : 0.f;
+          dz4[i] = valid[t] ? tp + tm : 0.f;
+          dwacc[t][4 * c + i] = valid[t] ? 0.f + (tp - tm) : 0.f;  // dense2: 0 + (tp - tm) per wave = tile
+        }
+        if (valid[t])
+          st4(GR(GR_DZ) + (R0 + rw[t]) * 64 + 16 * c + 4 * s4, make_float4(dz4[0], dz4[1], dz4[2], dz4[3]));
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dwacc[t][i] = row_sum16(dwacc[t][i]);
+    }
+    lds_barrier();  // every wave is done reading the G planes: the region becomes the dwa scratch
+    float* REDW = lds;  // [VNW][64]: one partial per tile slot (dense2: per wave = tile), zero past the tiles
+    if (c16 == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          st4(REDW + tl[t] * 64 + 16 * c + 4 * s4,
+              make_float4(dwacc[t][4 * c], dwacc[t][4 * c + 1], dwacc[t][4 * c + 2], dwacc[t][4 * c + 3]));
+    }
+    lds_barrier();
+    if (w == 0) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int k = 0; k < VNW; ++k) sacc += REDW[k * 64 + lane];
+      DWA[(size_t)blk * 64 + lane] = sacc;
+    }
+  }
+  ECO_TS(23);
+}
+
+static int mpnn_backward_dense3_launch(const MpnnArgs& a, hipStream_t st, int var) {
+  if (const int rc = dense3_check(a)) return rc;
+  const int blocks = (a.B + a.gpb - 1) / a.gpb;
+  if (var & 1) mpnn_backward_dense3_kernel<1><<<blocks, 64 * D3_NW, 0, st>>>(a);
+  else mpnn_backward_dense3_kernel<0><<<blocks, 64 * D3_NW, 0, st>>>(a);
+  return check_launch("mpnn_backward_dense3");
+}
+
 }  // namespace eco

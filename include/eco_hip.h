@@ -247,8 +247,9 @@ int eco_mpnn_forward_pair(const float *packed_a, const float *packed_b, int32_t 
  *   NO_DL     -- one-graph blocks of 224 < N <= 512 run the CSR-gather kernels;
  *   NO_SHARED -- N > 512 single-graph inference runs the per-episode global-memory kernel;
  *   NO_PAIR   -- eco_mpnn_forward_pair runs as two eco_mpnn_forward calls;
- *   DENSE2_FWD -- dense-aggregation forwards (N <= 224 blocks) run the one-tile-per-wave 16-wave kernel instead of
- *                 the two-tiles-per-wave 8-wave one (bitwise the same results; A/B and cross-check).
+ *   DENSE2_FWD -- dense-aggregation forwards and backwards (N <= 224 blocks) run the one-tile-per-wave 16-wave
+ *                 kernels instead of the two-tiles-per-wave 8-wave ones (bitwise the same results; A/B and
+ *                 cross-check).
  * The library reads no environment variables; this call is the only switch. Returns the previous mask. */
 enum { ECO_PATH_NO_DENSE = 1, ECO_PATH_NO_DL = 2, ECO_PATH_NO_SHARED = 4, ECO_PATH_NO_PAIR = 8, ECO_PATH_DENSE2_FWD = 16 };
 int32_t eco_set_kernel_paths(int32_t mask);
