@@ -108,10 +108,11 @@ __device__ __forceinline__ float wave_max_nonneg(float m) {
 }
 // max over the four lanes l, l^16, l^32, l^48 (one node of the node-operand layout) of a non-negative float
 __device__ __forceinline__ float node_max_nonneg(float m) {
+  // integer max: non-negative floats order as their bit patterns (fmaxf canonicalised both operands first)
   auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-  const float a = fmaxf(__uint_as_float(s16[0]), __uint_as_float(s16[1]));
-  auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-  return fmaxf(__uint_as_float(s32[0]), __uint_as_float(s32[1]));
+  const uint32_t a = max(s16[0], s16[1]);
+  auto s32 = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+  return __uint_as_float(max(s32[0], s32[1]));
 }
 // scale exponent k with max 2^k in [2^14, 2^15) (0 for an all-zero / non-finite max)
 __device__ __forceinline__ int scale_exp(float mx) {

@@ -192,6 +192,23 @@ __device__ __forceinline__ void lin128_2t(f32x4 (&acc)[2][4], const float4 (&xa0
   }
 }
 
+// The seven matrix scales kw (PK_FHS: Wf, then (Wm, Wu) per layer) as vector loads issued early; each use makes its
+// value wave-uniform (readfirstlane), so the load latency is waited for at the first use, not at the kernel start.
+struct KwLoad {
+  int v[FH_NMAT];
+  __device__ __forceinline__ explicit KwLoad(const float* P) {
+#pragma unroll
+    for (int m = 0; m < FH_NMAT; ++m) v[m] = fh_kw(P, m);
+  }
+  __device__ __forceinline__ int operator[](int m) const { return __builtin_amdgcn_readfirstlane(v[m]); }
+  __device__ __forceinline__ int message(int layer) const {
+    return __builtin_amdgcn_readfirstlane(layer == 0 ? v[1] : (layer == 1 ? v[3] : v[5]));
+  }
+  __device__ __forceinline__ int update(int layer) const {
+    return __builtin_amdgcn_readfirstlane(layer == 0 ? v[2] : (layer == 1 ? v[4] : v[6]));
+  }
+};
+
 __device__ __forceinline__ void zero_acc2(f32x4 (&d)[2][4]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -323,9 +340,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   auto net_body = [&](const MpnnArgs& a, const MpnnArgs* next, bool first) __attribute__((always_inline)) {
   const float* P = a.P;
   const uint16_t* PH = reinterpret_cast<const uint16_t*>(P + PK_FH);
-  int kw[FH_NMAT];  // the matrix scales, wave-uniform
-#pragma unroll
-  for (int m = 0; m < FH_NMAT; ++m) kw[m] = __builtin_amdgcn_readfirstlane(fh_kw(P, m));
+  KwLoad kw(P);  // the matrix scales: loaded here, made wave-uniform where they are used
   if (!first) {
     lin8_load(P + PK_WX, lane, wx8);
     lin8_load(P + PK_W0, lane, w08);
@@ -370,10 +385,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     f32x4 ea[2][4], ev[2][4];
     zero_acc2(ea);
     zero_acc2(ev);
-    if (act) {
-      AGG3(1, ea, PL, PL1, adjw, su, kc0, kc1, lane);
-      AGG3(2, ev, WB1, WB2, adjw, sv, kc0, kc1, lane);
-    }
+    AGG3(1, ea, PL, PL1, adjw, su, kc0, kc1, lane);
+    AGG3(2, ev, WB1, WB2, adjw, sv, kc0, kc1, lane);
     const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
     float4 acc[2][4];
     float sfx[2];
@@ -404,7 +417,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     }
     f32x4 d[2][4];
     zero_acc2(d);
-    if (act) mm_fh_2t(d, acc[0], acc[1], sfx, WB0, lane);
+    mm_fh_2t(d, acc[0], acc[1], sfx, WB0, lane);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       unscale(d[t], kx[t] + kw[0]);
@@ -453,6 +466,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   for (int layer = 0; layer < 3; ++layer) {
     const uint16_t* WM = layer == 0 ? WB1 : (layer == 1 ? WB0 : WB2);
     const uint16_t* WU = layer == 0 ? WB2 : (layer == 1 ? WB1 : WB0);
+    const int kwm = kw.message(layer);  // wave-uniform selects (a runtime index put kw[] in scratch memory)
+    const int kwu = kw.update(layer);
     if (layer == 1) {
       glds_frags<NW>(WB1, PH + FH_LAYER + FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu1
       glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_LAYER_STRIDE, 32, w, lane);            // Wm2
@@ -466,7 +481,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[t][kc]));  // no hoisting of the fragment masks
     f32x4 ag[2][4];
     zero_acc2(ag);
-    if (act) AGG3(0, ag, PL, PL1, adjw, sh, kc0, kc1, lane);
+    AGG3(0, ag, PL, PL1, adjw, sh, kc0, kc1, lane);
     float4 agg[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -475,6 +490,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       for (int c = 0; c < 4; ++c)
         agg[t][c] = make_float4(ag[t][c][0] * sc, ag[t][c][1] * sc, ag[t][c][2] * sc, ag[t][c][3] * sc);
     }
+    if (layer == 0) ECO_TS(10);
     glds_wait();
     lds_barrier();  // B1: planes read by every wave; this layer's weights landed
     if (layer == 0) ECO_TS(11);
@@ -499,17 +515,15 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         kx[t] = node_exp2(agg[t], ereg[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if (act) {
-        if constexpr (VAR & 2) {
-          lin128_2t(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
-        } else {
-          mm_fh_2t(d, ereg[0], ereg[1], sf, WM + FH_HALF, lane);
-          mm_fh_2t(d, agg[0], agg[1], sf, WM, lane);
-        }
+      if constexpr (VAR & 2) {
+        lin128_2t(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
+      } else {
+        mm_fh_2t(d, ereg[0], ereg[1], sf, WM + FH_HALF, lane);
+        mm_fh_2t(d, agg[0], agg[1], sf, WM, lane);
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        unscale(d[t], kx[t] + kw[1 + 2 * layer]);
+        unscale(d[t], kx[t] + kwm);
 #pragma unroll
         for (int c = 0; c < 4; ++c) mrel[t][c] = relu4(d[t][c]);
       }
@@ -536,17 +550,15 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         kx[t] = node_exp2(hreg[t], mrel[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if (act) {
-        if constexpr (VAR & 2) {
-          lin128_2t(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
-        } else {
-          mm_fh_2t(hn, hreg[0], hreg[1], sf, WU, lane);
-          mm_fh_2t(hn, mrel[0], mrel[1], sf, WU + FH_HALF, lane);
-        }
+      if constexpr (VAR & 2) {
+        lin128_2t(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
+      } else {
+        mm_fh_2t(hn, hreg[0], hreg[1], sf, WU, lane);
+        mm_fh_2t(hn, mrel[0], mrel[1], sf, WU + FH_HALF, lane);
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        unscale(hn[t], kx[t] + kw[2 + 2 * layer]);
+        unscale(hn[t], kx[t] + kwu);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           hreg[t][c] = valid[t] ? relu4(hn[t][c]) : zero4();
@@ -562,6 +574,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       for (int t = 0; t < 2; ++t)
         if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
     }
+    if (layer == 0) ECO_TS(14);
     lds_barrier();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
     ECO_TS(5 + layer);
   }
@@ -654,9 +667,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   }
   lds_barrier();
   float* Scr = reinterpret_cast<float*>(sW1);
-  const bool split = a.gpb < NW && readout_scratch_floats(rows_pad, a.gpb, NW, true) * 4 <= D2_WBUF_BYTES;
-  if (!split && readout_scratch_floats(rows_pad, a.gpb, NW, false) * 4 > D2_WBUF_BYTES) return;  // launch checks
-  readout_act<SAVE, NW>(a, Hs, D2_HS_LD, Scr, split, blk, g_valid, rows_valid, R0, RT);
+  // the readout's column sums in dense2's order: 16 strided partials (DN_NW virtual waves) when split
+  const bool split = a.gpb < DN_NW && readout_scratch_floats(rows_pad, a.gpb, DN_NW, true) * 4 <= D2_WBUF_BYTES;
+  if (!split && readout_scratch_floats(rows_pad, a.gpb, DN_NW, false) * 4 > D2_WBUF_BYTES) return;  // launch checks
+  readout_act<SAVE, NW, DN_NW>(a, Hs, D2_HS_LD, Scr, split, blk, g_valid, rows_valid, R0, RT);
   ECO_TS(8);
   if (next) lds_barrier();
   };  // net_body
@@ -667,7 +681,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
 static int dense3_check(const MpnnArgs& a) {
   const int rows_pad = (a.gpb * a.N + 15) & ~15;
   if (rows_pad > DN_MAX_ROWS || a.gpb > D2_MAX_GPB) return fail(ECO_ERR_ARG, "dense MPNN block exceeds the LDS tables");
-  if (readout_scratch_floats(rows_pad, a.gpb, D3_NW, false) * 4 > D2_WBUF_BYTES)
+  if (readout_scratch_floats(rows_pad, a.gpb, DN_NW, false) * 4 > D2_WBUF_BYTES)
     return fail(ECO_ERR_ARG, "dense MPNN readout scratch exceeds its buffer");
   return ECO_OK;
 }
@@ -679,8 +693,13 @@ static int mpnn_forward_dense3_launch_v(const MpnnArgs& a, bool save, hipStream_
   else mpnn_forward_dense3_kernel<false, 1, VAR><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
   return check_launch("mpnn_forward_dense3");
 }
+// var: the kernel-path bits 8-9 (eco_set_kernel_paths), A/B of the schedules -- bit 8 set: the aggregation without
+// the software pipeline (agg3), bit 9 set: the Linears without it (mm_fh_2t); default both pipelined (measured
+// fastest).  All four are bitwise equal.
+__host__ inline int dense3_variant(int var) { return (var & 3) ^ 3; }
 static int mpnn_forward_dense3_launch(const MpnnArgs& a, bool save, hipStream_t st, int var) {
   if (const int rc = dense3_check(a)) return rc;
+  var = dense3_variant(var);
   switch (var & 3) {
     case 1: return mpnn_forward_dense3_launch_v<1>(a, save, st);
     case 2: return mpnn_forward_dense3_launch_v<2>(a, save, st);
@@ -690,6 +709,7 @@ static int mpnn_forward_dense3_launch(const MpnnArgs& a, bool save, hipStream_t 
 }
 static int mpnn_forward_dense3_pair_launch(const MpnnArgs& a, const MpnnArgs& b, hipStream_t st, int var) {
   if (const int rc = dense3_check(a)) return rc;
+  var = dense3_variant(var);
   if (a.gpb != 1) return fail(ECO_ERR_ARG, "paired dense forward: one graph per block only");
   switch (var & 3) {
     case 1: mpnn_forward_dense3_kernel<false, 2, 1><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
@@ -783,9 +803,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   float* DWA = DBR + ((a.B + 63) & ~63);  // [nblocks][64]
   auto WUT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE + 2 * FH_HALF; };  // Wu^T: 2 output halves
   auto WMT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE; };                // Wm^T: dagg, de halves
-  int kw[FH_NMAT];
-#pragma unroll
-  for (int m = 0; m < FH_NMAT; ++m) kw[m] = __builtin_amdgcn_readfirstlane(fh_kw(P, m));
+  KwLoad kw(P);  // the matrix scales: loaded here, made wave-uniform where they are used
 
   // ---- staging: Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (LDS-DMA), row info, edge bases ----
   glds_frags<NW>(WB0, WUT(2), 32, w, lane);
@@ -827,20 +845,21 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
   lds_barrier();
   if (split) {  // dWr[64:] = sum_v dq_v h3_v, over dense2's 16 strided partial sums (virtual waves w, w + 8)
+    ECO_TS(29);
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* h3 = SV(SV_H3) + (R0 + (size_t)gl * N) * 64;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int vw = w + NW * u;
-        float dwb = 0.f;
-        for (int v = vw; v < N; v += VNW) {
-          const float dv = DQ[gl * N + v];
-          if (dv != 0.f) dwb = fmaf(dv, h3[(size_t)v * 64 + lane], dwb);
-        }
-        RED[(gl * VNW + vw) * 64 + lane] = dwb;
+      float dwb0 = 0.f, dwb1 = 0.f;  // virtual waves w and w + NW, interleaved
+      for (int v = w; v < N; v += VNW) {
+        const float dv0 = DQ[gl * N + v];
+        const float dv1 = v + NW < N ? DQ[gl * N + v + NW] : 0.f;
+        if (dv0 != 0.f) dwb0 = fmaf(dv0, h3[(size_t)v * 64 + lane], dwb0);
+        if (dv1 != 0.f) dwb1 = fmaf(dv1, h3[(size_t)(v + NW) * 64 + lane], dwb1);
       }
+      RED[(gl * VNW + w) * 64 + lane] = dwb0;
+      RED[(gl * VNW + w + NW) * 64 + lane] = dwb1;
     }
     lds_barrier();
+    ECO_TS(30);
   }
   for (int gl = w; gl < g_valid; gl += NW) {
     const int e = blk * a.gpb + gl;
@@ -871,6 +890,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
     DWRB[(size_t)e * 64 + lane] = dwb;
   }
   lds_barrier();
+  ECO_TS(31);
   // dh3 (node-operand layout): dq_i * wr[64+f] + dmean_f / N
   float4 dh[2][4];
 #pragma unroll
@@ -899,6 +919,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   for (int layer = 2; layer >= 0; --layer) {
     const uint16_t* WU = layer == 2 ? WB0 : (layer == 1 ? WB2 : WB1);
     const uint16_t* WM = layer == 2 ? WB1 : (layer == 1 ? WB0 : WB2);
+    const int kwm = kw.message(layer);
+    const int kwu = kw.update(layer);
     // duu = dh' * [h' > 0]  (in place in dh)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -921,10 +943,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         kx[t] = node_exp<4>(dh[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if (act) mm_fh2_2t(dhd, dmm, dh[0], dh[1], sf, WU, WU + FH_HALF, lane);
+      mm_fh2_2t(dhd, dmm, dh[0], dh[1], sf, WU, WU + FH_HALF, lane);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int ku = kx[t] + kw[2 + 2 * layer];
+        const int ku = kx[t] + kwu;
         unscale(dhd[t], ku);
         unscale(dmm[t], ku);
         const uint32_t mmask = mask16(rmask[t], SM_M0 + layer);
@@ -958,10 +980,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         kx[t] = node_exp<4>(dum[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if (act) mm_fh2_2t(dg, dd, dum[0], dum[1], sf, WM, WM + FH_HALF, lane);
+      mm_fh2_2t(dg, dd, dum[0], dum[1], sf, WM, WM + FH_HALF, lane);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int km = kx[t] + kw[1 + 2 * layer];
+        const int km = kx[t] + kwm;
         unscale(dg[t], km);
         unscale(dd[t], km);
         float4 g[4];
@@ -994,7 +1016,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         for (int kc = 0; kc < DN_KC; ++kc) asm volatile("" : "+v"(adjw[t][kc]));
       f32x4 ag[2][4];
       zero_acc2(ag);
-      if (act) AGG3(0, ag, PL, PL1, adjw, sg, kc0, kc1, lane);
+      AGG3(0, ag, PL, PL1, adjw, sg, kc0, kc1, lane);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1036,7 +1058,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
       kx[t] = node_exp<4>(due[t]);
       sf[t] = exp2i(kx[t]);
     }
-    if (act) mm_fh_2t(dg, due[0], due[1], sf, WB0, lane);
+    mm_fh_2t(dg, due[0], due[1], sf, WB0, lane);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       unscale(dg[t], kx[t] + kw[0]);
@@ -1072,10 +1094,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
     f32x4 gp[2][4], gm[2][4];
     zero_acc2(gp);
     zero_acc2(gm);
-    if (act) {
-      AGG3(1, gp, PL, PL1, adjw, sg, kc0, kc1, lane);
-      AGG3(2, gm, PL, PL1, adjw, sg, kc0, kc1, lane);
-    }
+    AGG3(1, gp, PL, PL1, adjw, sg, kc0, kc1, lane);
+    AGG3(2, gm, PL, PL1, adjw, sg, kc0, kc1, lane);
     float dwacc[2][16];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1123,6 +1143,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
 
 static int mpnn_backward_dense3_launch(const MpnnArgs& a, hipStream_t st, int var) {
   if (const int rc = dense3_check(a)) return rc;
+  var = dense3_variant(var);
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
   if (var & 1) mpnn_backward_dense3_kernel<1><<<blocks, 64 * D3_NW, 0, st>>>(a);
   else mpnn_backward_dense3_kernel<0><<<blocks, 64 * D3_NW, 0, st>>>(a);

@@ -202,24 +202,29 @@ __host__ __device__ constexpr int readout_scratch_floats(int rows_pad, int gpb, 
 template <int NW>
 __device__ __forceinline__ void graph_act(const MpnnArgs& a, const float* Qb, int blk, int g_valid, size_t R0);
 
-template <bool SAVE, int NW>
+// VNW (>= NW, a multiple of it): the number of strided column-sum partials when `split` -- the summation order of a
+// kernel with VNW waves, kept by a kernel with fewer (mpnn_forward_dense3_kernel: 8 waves, dense2's 16 partials).
+template <bool SAVE, int NW, int VNW = NW>
 __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, int ldh, float* Scr, bool split,
                                             int blk, int g_valid, int rows_valid, size_t R0, size_t RT) {
+  static_assert(VNW % NW == 0, "virtual waves: a multiple of the waves");
   constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63;
   const int w = uniform_i(threadIdx.x >> 6);
   const int N = a.N;
   const float* P = a.P;
   // column sums: all waves on each graph when there are fewer graphs than waves, else one wave per graph
-  float* Red = Scr;                                   // [gpb][NW][64] column-sum partials (split)
-  float* CG = Red + (split ? a.gpb * NW * 64 : 0);   // [gpb] relu(p) . wr[:64]
+  float* Red = Scr;                                   // [gpb][VNW][64] column-sum partials (split)
+  float* CG = Red + (split ? a.gpb * VNW * 64 : 0);  // [gpb] relu(p) . wr[:64]
   float* Qb = CG + ((a.gpb + 3) & ~3);               // [rows_pad] q values
   if (split) {
     for (int gl = 0; gl < g_valid; ++gl) {
       const float* hg = Hs + gl * N * ldh;
-      float cs = 0.f;
-      for (int v = w; v < N; v += NW) cs += hg[v * ldh + lane];
-      Red[(gl * NW + w) * 64 + lane] = cs;
+      for (int vw = w; vw < VNW; vw += NW) {
+        float cs = 0.f;
+        for (int v = vw; v < N; v += VNW) cs += hg[v * ldh + lane];
+        Red[(gl * VNW + vw) * 64 + lane] = cs;
+      }
     }
     __syncthreads();
   }
@@ -228,7 +233,7 @@ __device__ __forceinline__ void readout_act(const MpnnArgs& a, const float* Hs, 
     float cs = 0.f;
     if (split) {
 #pragma unroll
-      for (int k = 0; k < NW; ++k) cs += Red[(gl * NW + k) * 64 + lane];  // fixed order
+      for (int k = 0; k < VNW; ++k) cs += Red[(gl * VNW + k) * 64 + lane];  // fixed order
     } else {
       const float* hg = Hs + gl * N * ldh;
       for (int v = 0; v < N; ++v) cs += hg[v * ldh + lane];

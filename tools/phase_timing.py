@@ -54,7 +54,9 @@ def main():
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--p", type=float, default=0.15, help="ER p, or BA m with --graph BA")
     ap.add_argument("--graph", default="ER", choices=["ER", "BA"])
+    ap.add_argument("--paths", type=int, default=0, help="eco_set_kernel_paths mask (16: the 16-wave dense2 kernels)")
     args = ap.parse_args()
+    _lib.lib.eco_set_kernel_paths(args.paths)
     dev = torch.device("cuda:0")
     B, N = args.batch, args.n
     store = GraphStore.generated(args.graph, B, N, args.p if args.graph == "ER" else int(args.p), seed=1, device=dev)
@@ -84,7 +86,7 @@ def main():
         elif os.environ.get("ECO_DENSE_V1"):
             report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
                    ["weight staging", "MFMA half 1 issue", "gather", "MFMA half 2", "(drain)", "to barrier"])
-        else:  # mpnn_forward_dense2_kernel
+        else:  # mpnn_forward_dense2_kernel / dense3 (wave 0's first tile)
             report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
                    ["aggregation", "B1 wait", "message", "update", "h' planes", "B2 wait"])
     q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
@@ -97,6 +99,9 @@ def main():
     torch.cuda.synchronize()
     ts = stamps(nblk)
     report(f"backward          B={B} N={N}", ts, list(range(16, 24)), BWD)
+    if ts is not None and ts[:, 29].any():  # mpnn_backward_dense3_kernel's readout
+        report("  readout detail (wave 0)", ts, [17, 29, 30, 31, 18],
+               ["DQ staging", "dq . h3 sums", "per-graph (wave 0)", "dh3 + DMA wait + pad"])
     if ts is not None and ts[:, 24].any():
         if dl:
             report("  layer 1 detail (wave 0)", ts, [19, 24, 20], ["Linears + lo planes", "barrier + agg lo/hi"])
