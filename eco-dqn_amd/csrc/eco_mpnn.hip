@@ -1356,22 +1356,45 @@ __device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], 
   const uint16_t* wl = WH + lane * 8;
 #pragma unroll
   for (int kc2 = 0; kc2 < 2; ++kc2) {
-    f16x8 xh, xl;
-    probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+    f16x8 w1[4], w2[4];  // weight fragments read first: nothing but the split sits between it and the MFMAs
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const f16x8 w1 = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
-      const f16x8 w2 = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
-      if (ORDER == 0) {  // mm_fh
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
+      w1[nt] = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
+      w2[nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
+    }
+    if (ORDER == 1) {
+      // order 1 places the lo fragment's first reader straight after the split's last v_fma_mixhi: all loads
+      // drained and earlier MFMAs retired first (nothing for the compiler to interleave), then that first
+      // MFMA as inline asm (so no compiler-inserted wait state can separate it from the asm split), followed by
+      // enough s_nop for every MFMA result hazard the recognizer cannot see through asm
+      __builtin_amdgcn_s_waitcnt(0);
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f16x8 xh, xl;
+    probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+    if (ORDER == 1) {
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                   : "+v"(acc[0])
+                   : "v"(w1[0]), "v"(xl));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      if (ORDER == 1 && nt == 0) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[0], xh, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[0], xh, acc[0], 0, 0, 0);
+      } else if (ORDER == 0) {  // mm_fh
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[nt], xh, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], xl, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], xh, acc[nt], 0, 0, 0);
       } else {
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xl, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2, xh, acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, xh, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], xl, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[nt], xh, acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[nt], xh, acc[nt], 0, 0, 0);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 template <int ORDER>

@@ -22,6 +22,27 @@
 namespace eco {
 
 constexpr int D3_NW = 8;  // waves per workgroup
+
+// LDS byte address of a plane element, made opaque to the compiler: the fragment reads then address it as one
+// register plus immediate offsets (< 64 KB) instead of one v_or of the lane part with a >16-bit constant per read
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+__device__ __forceinline__ uint32_t lds_base(const uint16_t* p) {
+  uint32_t b = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
+#ifndef ECO_D3_PLAIN_ADDR  // (A/B: the compiler's own addressing)
+  asm volatile("" : "+v"(b));
+#endif
+  return b;
+}
+__device__ __forceinline__ v4s tr_read_at(uint32_t b, int bytes) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(size_t)(b + (uint32_t)bytes));
+}
+// the (lo, hi) fragment pair of plane base b, chunk kc, feature block ft (the lane part is in b)
+__device__ __forceinline__ f16x8 plane_frag(uint32_t b, int kc, int ft) {
+  const int o = 2 * (32 * kc * 16 + ft * (DN_KPMAX * 16));
+  const v4s lo = tr_read_at(b, o), hi = tr_read_at(b, o + 2 * 16 * 16);
+  const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(f16x8, raw);
+}
 // aggregation of the wave's two tiles: the pipelined straight-line form when every chunk is live (VAR bit 0)
 #define AGG3(M, acc, P0, P1, adjw, sc, kc0, kc1, lane)                                        \
   do {                                                                                      \
@@ -39,6 +60,7 @@ __device__ __forceinline__ void agg3(f32x4 (&acc)[2][4], const uint16_t* P0, con
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;
+  const uint32_t pb[2] = {lds_base(P0 + j_in * 16 + 4 * pc), lds_base(P1 + j_in * 16 + 4 * pc)};
 #pragma unroll
   for (int kc = 0; kc < DN_KC; ++kc) {
     if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
@@ -46,17 +68,11 @@ __device__ __forceinline__ void agg3(f32x4 (&acc)[2][4], const uint16_t* P0, con
     const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
     const f16x8 b0 = adj_frag2<MODE>(adjw[0][kc], plo, phi);
     const f16x8 b1 = adj_frag2<MODE>(adjw[1][kc], plo, phi);
-    const int off = (32 * kc + j_in) * 16 + 4 * pc;
     f16x8 af[2][4];
 #pragma unroll
     for (int p = 1; p >= 0; --p) {
 #pragma unroll
-      for (int ft = 0; ft < 4; ++ft) {
-        const uint16_t* a = (p ? P1 : P0) + off + ft * (DN_KPMAX * 16);
-        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
-        const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[p][ft] = __builtin_bit_cast(f16x8, raw);
-      }
+      for (int ft = 0; ft < 4; ++ft) af[p][ft] = plane_frag(pb[p], kc, ft);
     }
 #pragma unroll
     for (int p = 1; p >= 0; --p) {  // the small plane first (dense2's order per accumulator)
@@ -80,18 +96,13 @@ __device__ __forceinline__ void agg3f(f32x4 (&acc)[2][4], const uint16_t* P0, co
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;
+  const uint32_t pb[2] = {lds_base(P0 + j_in * 16 + 4 * pc), lds_base(P1 + j_in * 16 + 4 * pc)};
   f16x8 fa[2][8], fb[2][2];
   auto issue = [&](int kc, int buf) {
-    const int off = (32 * kc + j_in) * 16 + 4 * pc;
 #pragma unroll
     for (int p = 1; p >= 0; --p) {
 #pragma unroll
-      for (int ft = 0; ft < 4; ++ft) {
-        const uint16_t* a = (p ? P1 : P0) + off + ft * (DN_KPMAX * 16);
-        const v4s lo = tr_read(a), hi = tr_read(a + 16 * 16);
-        const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        fa[buf][(1 - p) * 4 + ft] = __builtin_bit_cast(f16x8, raw);
-      }
+      for (int ft = 0; ft < 4; ++ft) fa[buf][(1 - p) * 4 + ft] = plane_frag(pb[p], kc, ft);
     }
     const uint32_t plo = __builtin_amdgcn_readlane(sc.pat, 2 * kc);
     const uint32_t phi = __builtin_amdgcn_readlane(sc.pat, 2 * kc + 1);
@@ -373,7 +384,9 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       }
     }
   }
+  ECO_TS(9);
   glds_wait();  // Wf fragments
+  ECO_TS(15);
   lds_barrier();
   ECO_TS(2);
 

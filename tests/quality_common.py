@@ -50,8 +50,9 @@ def family_graphs(kind, n, seed):
     return [og.ba_graph(n, 4, rng) for _ in range(N_GRAPHS)]
 
 
-def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048):
-    """The benched agent trained by learn(); returns (the `_best` network, info)."""
+def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048, configure=None):
+    """The benched agent trained by learn(); returns (the `_best` network, info).  configure: optional callable on
+    the agent before training (tools/r05/quality_sweep.py)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.networks.mpnn import MPNN
@@ -68,6 +69,8 @@ def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048):
     agent.network_save_path = os.path.join(tmp, "net.pth")
     agent.test_save_path = os.path.join(tmp, "test_scores")
     agent.save_network_frequency = 10 ** 12
+    if configure is not None:
+        configure(agent)
     t0 = time.perf_counter()
     agent.learn(timesteps=steps)
     torch.cuda.synchronize()

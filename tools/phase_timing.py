@@ -89,6 +89,9 @@ def main():
         else:  # mpnn_forward_dense2_kernel / dense3 (wave 0's first tile)
             report("  layer 0 detail (wave 0)", ts, [4, 10, 11, 12, 13, 14, 5],
                    ["aggregation", "B1 wait", "message", "update", "h' planes", "B2 wait"])
+    if ts is not None and ts[:, 9].any():  # dense3: the prologue in detail (wave 0)
+        report("  prologue detail (wave 0)", ts, [0, 1, 9, 15, 2],
+               ["staging loads", "phase A compute + planes", "Wf DMA wait", "barrier"])
     q = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, saved=saved)
     torch.cuda.synchronize()
     report(f"forward (save)    B={B} N={N}", stamps(nblk), list(range(0, 9)), fwd_names)
