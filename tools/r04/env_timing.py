@@ -20,8 +20,8 @@ from eco_hip.graphs import GraphStore  # noqa: E402
 from eco_hip.envs.batched import VecSpinSystem  # noqa: E402
 from eco_hip.envs.utils import DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget  # noqa: E402
 
-NAMES = ["record, row bounds, state rows, edges", "table gathers + field update", "flip, ballots, history",
-         "reward, best", "writes (observation rows, state, record)"]
+NAMES = ["scalars + state rows", "CSR row + field update", "flip, ballots, history", "reward, best, writes",
+         "observation rows"]
 
 
 def main():
