@@ -1374,9 +1374,16 @@ __device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], 
     f16x8 xh, xl;
     probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
     if (ORDER == 1) {
-      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
-                   : "+v"(acc[0])
-                   : "v"(w1[0]), "v"(xl));
+      // (the plain-conversion reference split is compiler VALU code: its wait states before this asm MFMA are
+      // written out here, the recognizer not knowing the asm is an MFMA; the asm split carries its own)
+      if (REF)
+        asm volatile("s_nop 4\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                     : "+v"(acc[0])
+                     : "v"(w1[0]), "v"(xl));
+      else
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                     : "+v"(acc[0])
+                     : "v"(w1[0]), "v"(xl));
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll

@@ -23,15 +23,12 @@ namespace eco {
 
 constexpr int D3_NW = 8;  // waves per workgroup
 
-// LDS byte address of a plane element, made opaque to the compiler: the fragment reads then address it as one
-// register plus immediate offsets (< 64 KB) instead of one v_or of the lane part with a >16-bit constant per read
+// LDS byte address of a plane element.  (Making it opaque -- one base register plus immediate offsets per
+// fragment read instead of the compiler's v_or of the lane part with a >16-bit constant -- removed ~220 VALU from
+// the kernel and measured no faster: 0.7007-0.703 vs 0.6976-0.6987 ms per M = 2048 launch, profiles/r05/.)
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 __device__ __forceinline__ uint32_t lds_base(const uint16_t* p) {
-  uint32_t b = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
-#ifndef ECO_D3_PLAIN_ADDR  // (A/B: the compiler's own addressing)
-  asm volatile("" : "+v"(b));
-#endif
-  return b;
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
 }
 __device__ __forceinline__ v4s tr_read_at(uint32_t b, int bytes) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(size_t)(b + (uint32_t)bytes));
