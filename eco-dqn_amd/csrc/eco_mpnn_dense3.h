@@ -228,12 +228,11 @@ __device__ __forceinline__ void zero_acc2(f32x4 (&d)[2][4]) {
 // graph per block with a prepared gs.adjbits: per-lane loads; otherwise row info / edge bases / max degrees in LDS
 // and the block bitmask built once (barriers: uniform over the workgroup).
 template <int NT>
-__device__ __forceinline__ void d3_stage(const MpnnArgs& a, int blk, int rows_pad, int rows_valid, const int (&r)[2],
-                                         const bool (&valid)[2], int s4, int2* RI, int64_t* GB, int* MD,
-                                         uint32_t* ADJ, float (&nf)[2], int (&md)[2],
-                                         uint32_t (&adjw)[2][DN_KC]) {
+__device__ __forceinline__ void d3_stage_raw(const MpnnArgs& a, int blk, int rows_pad, int rows_valid,
+                                             const int (&r)[2], const bool (&valid)[2], int s4, int2* RI, int64_t* GB,
+                                             int* MD, uint32_t* ADJ, float (&nf)[2], int (&md)[2],
+                                             uint32_t (&adjb)[2][4]) {
   const int N = a.N;
-  uint32_t adjb[2][4];
   if (a.gpb == 1 && a.gs.adjbits != nullptr) {
     const int gid = a.gids[blk];  // uniform: scalar load
     const int mdg = a.gs.max_deg[gid];
@@ -265,10 +264,23 @@ __device__ __forceinline__ void d3_stage(const MpnnArgs& a, int blk, int rows_pa
     }
     if (built) __syncthreads();
   }
+}
+// the bitmask words as the spread words of agg3 (the first use of the staged adjacency: placing it late lets the
+// adjacency / degree loads of the prepared-bitmask path run under the forward's phase A)
+__device__ __forceinline__ void d3_spread(const uint32_t (&adjb)[2][4], uint32_t (&adjw)[2][DN_KC]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int kc = 0; kc < DN_KC; ++kc) adjw[t][kc] = adj_spread((adjb[t][kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
+}
+template <int NT>
+__device__ __forceinline__ void d3_stage(const MpnnArgs& a, int blk, int rows_pad, int rows_valid, const int (&r)[2],
+                                         const bool (&valid)[2], int s4, int2* RI, int64_t* GB, int* MD,
+                                         uint32_t* ADJ, float (&nf)[2], int (&md)[2],
+                                         uint32_t (&adjw)[2][DN_KC]) {
+  uint32_t adjb[2][4];
+  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, RI, GB, MD, ADJ, nf, md, adjb);
+  d3_spread(adjb, adjw);
 }
 
 // LDS (ECO_D2_LDS), as mpnn_forward_dense2_kernel.  NNET = 2: the online and the target network on the same graphs
@@ -333,12 +345,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   for (int c = 0; c < 4; ++c) wa4[c] = f4(P + PK_WA + 16 * c + 4 * s4);
   float nf[2];
   int md_graph[2];
-  uint32_t adjw[2][DN_KC];
-  d3_stage<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, sRI, sGB, sMD, ADJ, nf, md_graph, adjw);
+  uint32_t adjb[2][4], adjw[2][DN_KC];
+  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, sRI, sGB, sMD, ADJ, nf, md_graph, adjb);
   ECO_TS(1);
   float rnf[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
   // aggregation chunks of the wave's rows (the union of its two tiles' ranges)
   const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
@@ -386,6 +396,11 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   ECO_TS(15);
   lds_barrier();
   ECO_TS(2);
+  if (first) {  // the staged adjacency and degrees, first needed here
+    d3_spread(adjb, adjw);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
+  }
 
   // ---- phase B: edge embedding (mpnn.py:89-104): (A+ . relu(Z + w_a) + A- . relu(Z - w_a)) / norm; Wf ----
   float4 ereg[2][4];
@@ -630,6 +645,16 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
           st4(COL + tl[t] * 64 + 16 * c + 4 * s4, make_float4(cs[4 * c], cs[4 * c + 1], cs[4 * c + 2], cs[4 * c + 3]));
       }
     }
+    // wave 0's readout weights (its Wp row, Wr[lane], b) in flight across the barrier
+    float4 wpv[16];
+    float wr_l = 0.f, br = 0.f;
+    if (w == 0) {
+      const float* wp = P + PK_WP + lane * 64;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) wpv[k] = f4(wp + 4 * k);
+      wr_l = P[PK_WR + lane];
+      br = P[PK_BR];
+    }
     lds_barrier();
     if (w == 0) {
       float cs = 0.f;
@@ -637,11 +662,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       const float mean = cs / (float)N;
       MEANS[lane] = mean;
       wave_lds_sync();
-      const float* wp = P + PK_WP + lane * 64;
       float p = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const float4 wv = f4(wp + 4 * k), mv = f4(MEANS + 4 * k);
+        const float4 wv = wpv[k], mv = f4(MEANS + 4 * k);
         p = fmaf(wv.x, mv.x, p);
         p = fmaf(wv.y, mv.y, p);
         p = fmaf(wv.z, mv.z, p);
@@ -651,8 +675,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)blk * 64 + lane] = mean;
         a.sv[(size_t)SV_NODE_TENSORS * RT * 64 + (size_t)a.B * 64 + (size_t)blk * 64 + lane] = p;
       }
-      const float cg = wave_sum_f(relu(p) * P[PK_WR + lane]);
-      const float br = P[PK_BR];
+      const float cg = wave_sum_f(relu(p) * wr_l);
       for (int i = lane; i < N; i += 64) {
         const float qv = cg + QL[i] + br;
         QB[i] = qv;

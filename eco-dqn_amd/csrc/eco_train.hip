@@ -23,6 +23,9 @@ struct WJob {
   int out_col0;      // first column in the flat buffer
 };
 constexpr int MAX_JOBS = 10;
+#ifndef WGRAD_NT
+#define WGRAD_NT 0  // A/B: nontemporal (streaming) loads of the dY / X rows
+#endif
 constexpr int WGRAD_WG_X = 3;  // workgroups per CU over all jobs (46 KB LDS each: 3 resident per CU)
 constexpr int WG_PER_JOB = 128;
 constexpr int SLABS_PER_JOB = WG_PER_JOB;  // one [64][128] partial per workgroup
@@ -110,6 +113,15 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
   // raw loads only; the row / column masks are applied when the tile is stored (masking at load
   // time makes the compiler wait for every load before the multiply it should overlap)
   auto load_tile = [&](Regs& R, int rb) {
+#if WGRAD_NT
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R.y[k] = __builtin_nontemporal_load(&ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64]);
+#pragma unroll
+    for (int u = 0; u < XU; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        R.x[u][k] = __builtin_nontemporal_load(&xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld]);
+#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) R.y[k] = ysrc[(size_t)min(rb + 8 * yg + k, rlast) * 64];
 #pragma unroll
@@ -117,6 +129,7 @@ __device__ __forceinline__ void wgrad_bf3_job(const WJobs& jobs, float* slabs, i
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         R.x[u][k] = xg[(size_t)min(rb + 8 * (xg0 + XG * u) + k, rlast) * (size_t)xld];
+#endif
   };
   auto store_tile = [&](Regs& R, int rb) {
     asm volatile("" : "+s"(rb));  // keeps the masking (and this tile's wait) at the store
