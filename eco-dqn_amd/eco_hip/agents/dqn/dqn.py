@@ -511,8 +511,7 @@ class DQN:
                     e["net"] = e["p"]["net"]
                 else:
                     e["result"] = self.evaluate_agent()
-                    e["net"] = self.network
-            if rank == 0 and owner != rank:  # the weights at tk, for _best
+            if rank == 0 and e["net"] is None:  # the weights at tk, for _best (recorded after more training)
                 snap = self._network_factory()
                 snap.flat.copy_(self.network.flat)
                 e["net"] = snap
