@@ -16,10 +16,6 @@
 
 namespace eco {
 
-#ifndef ENV_NT_OBS
-#define ENV_NT_OBS 0
-#endif
-
 // ------------------------------------------------------------------ graphs ----
 // score_solver.py:347-375 (normalisers) and mpnn.py:34-38 (degree norm).
 // The graph's edge words are streamed ONCE, coalesced (thread t of the graph reads edges t, t + 64 WPG,
@@ -190,14 +186,8 @@ __device__ __forceinline__ void write_obs_default(const EnvArgs& a, int e, int l
     const float x1 = __fdiv_rn(sf * (float)h[k], mlrf);
     const float x2 = (float)tab[tsf[k]];
     float4* dst = (float4*)(a.obs_x + ((size_t)e * N + v) * 8);
-#if ENV_NT_OBS  // A/B: streaming (nontemporal) stores of the feature rows
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(f4v{x0, x1, x2, u3}, reinterpret_cast<f4v*>(dst));
-    __builtin_nontemporal_store(f4v{u4, u5, u6, 0.f}, reinterpret_cast<f4v*>(dst) + 1);
-#else
     dst[0] = make_float4(x0, x1, x2, u3);
     dst[1] = make_float4(u4, u5, u6, 0.f);
-#endif
   }
 }
 

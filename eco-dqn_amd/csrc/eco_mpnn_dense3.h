@@ -22,6 +22,9 @@
 namespace eco {
 
 constexpr int D3_NW = 8;  // waves per workgroup
+#ifndef D3_LIN_SPLIT_AHEAD
+#define D3_LIN_SPLIT_AHEAD 1  // A/B: the inference forward's Linears split one step ahead
+#endif
 
 // LDS byte address of a plane element.  (Making it opaque -- one base register plus immediate offsets per
 // fragment read instead of the compiler's v_or of the lane part with a >16-bit constant -- removed ~220 VALU from
@@ -160,6 +163,7 @@ __device__ __forceinline__ void mm_fh_2t(f32x4 (&acc)[2][4], const float4 (&x0)[
 // accumulator in the same order), software-pipelined over its four 32-input steps: step s + 1's eight weight
 // fragments are read while step s's inputs are split and its 24 MFMAs run (sched_barrier keeps each step's reads
 // ahead of their MFMAs instead of right before them).
+template <bool AHEAD>
 __device__ __forceinline__ void lin128_2t(f32x4 (&acc)[2][4], const float4 (&xa0)[4], const float4 (&xa1)[4],
                                           const uint16_t* WA, const float4 (&xb0)[4], const float4 (&xb1)[4],
                                           const uint16_t* WB, const float (&sf)[2], int lane) {
@@ -173,6 +177,49 @@ __device__ __forceinline__ void lin128_2t(f32x4 (&acc)[2][4], const float4 (&xa0
       w2[buf][nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
     }
   };
+if constexpr (AHEAD) {
+  // the inputs of step s + 1 are split while step s's MFMAs run (VALU under the matrix core, one wave); the
+  // second split set costs 16 VGPRs: the inference forward only (the saving and the paired kernels would spill)
+  f16x8 xs[2][4];  // [buf][xh0, xl0, xh1, xl1]
+  auto split_step = [&](int s, int buf) {
+    const int kc2 = s & 1;
+    if (s < 2) {
+      split_fh(xa0[2 * kc2], xa0[2 * kc2 + 1], sf[0], xs[buf][0], xs[buf][1]);
+      split_fh(xa1[2 * kc2], xa1[2 * kc2 + 1], sf[1], xs[buf][2], xs[buf][3]);
+    } else {
+      split_fh(xb0[2 * kc2], xb0[2 * kc2 + 1], sf[0], xs[buf][0], xs[buf][1]);
+      split_fh(xb1[2 * kc2], xb1[2 * kc2 + 1], sf[1], xs[buf][2], xs[buf][3]);
+    }
+  };
+  issue(0, 0);
+  split_step(0, 0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < 4) {
+      issue(s + 1, cur ^ 1);
+      split_step(s + 1, cur ^ 1);
+    }
+    const f16x8 xh0 = xs[cur][0], xl0 = xs[cur][1], xh1 = xs[cur][2], xl1 = xs[cur][3];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[cur][nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[cur][nt], xh1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xl0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xl1, acc[1][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xh0, acc[0][nt], 0, 0, 0);
+      acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[cur][nt], xh1, acc[1][nt], 0, 0, 0);
+    }
+    if (s + 1 < 4) {
+#pragma unroll
+      for (int i = 0; i < 24; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU (the next step's split)
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+} else {
   issue(0, 0);
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -198,6 +245,7 @@ __device__ __forceinline__ void lin128_2t(f32x4 (&acc)[2][4], const float4 (&xa0
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+}
 }
 
 // The seven matrix scales kw (PK_FHS: Wf, then (Wm, Wu) per layer) as vector loads issued early; each use makes its
@@ -541,7 +589,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         sf[t] = exp2i(kx[t]);
       }
       if constexpr (VAR & 2) {
-        lin128_2t(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
+        lin128_2t<D3_LIN_SPLIT_AHEAD && !SAVE && NNET == 1>(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
       } else {
         mm_fh_2t(d, ereg[0], ereg[1], sf, WM + FH_HALF, lane);
         mm_fh_2t(d, agg[0], agg[1], sf, WM, lane);
@@ -576,7 +624,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         sf[t] = exp2i(kx[t]);
       }
       if constexpr (VAR & 2) {
-        lin128_2t(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
+        lin128_2t<D3_LIN_SPLIT_AHEAD && !SAVE && NNET == 1>(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
       } else {
         mm_fh_2t(hn, hreg[0], hreg[1], sf, WU, lane);
         mm_fh_2t(hn, mrel[0], mrel[1], sf, WU + FH_HALF, lane);
@@ -855,10 +903,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   }
   float nf[2], rnf[2];
   int md_unused[2];
-  uint32_t adjw[2][DN_KC];
-  d3_stage<NT>(a, blk, rows_pad, rows_valid, rw, valid, s4, sRI, sGB, sMD, ADJ, nf, md_unused, adjw);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
+  uint32_t adjb[2][4], adjw[2][DN_KC];
+  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, rw, valid, s4, sRI, sGB, sMD, ADJ, nf, md_unused, adjb);
   const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
@@ -876,6 +922,14 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   float* RED = DMEAN + a.gpb * 64;       // [gpb][VNW][64] (split)
   const bool split = a.gpb < VNW && (size_t)(rows_pad + a.gpb * 64 + a.gpb * VNW * 64) * 4 <= (size_t)D2_PL_BYTES;
   for (int i = threadIdx.x; i < rows_pad; i += NT) DQ[i] = i < rows_valid ? a.dq[R0 + i] : 0.f;
+  // the per-graph waves' Wp columns (Wp[k][lane], k < 64) and p, loaded ahead: the dmean chain below then runs on
+  // registers instead of waiting on 64 dependent-order L2 reads (same FMAs, same order)
+  float wpk[64], p_pre = 0.f;
+  if (w < g_valid) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) wpk[k] = P[PK_WP + k * 64 + lane];
+    p_pre = PP[(size_t)(blk * a.gpb + w) * 64 + lane];
+  }
   lds_barrier();
   if (split) {  // dWr[64:] = sum_v dq_v h3_v, over dense2's 16 strided partial sums (virtual waves w, w + 8)
     ECO_TS(29);
@@ -899,15 +953,22 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
     float sacc = 0.f;
     for (int v = lane; v < N; v += 64) sacc += DQ[gl * N + v];
     const float S = wave_sum_f(sacc);
-    const float p = PP[(size_t)e * 64 + lane];
+    const float p = gl == w ? p_pre : PP[(size_t)e * 64 + lane];
     const float dp = P[PK_WR + lane] * S * (p > 0.f ? 1.f : 0.f);
     DP[(size_t)e * 64 + lane] = dp;
     DWRA[(size_t)e * 64 + lane] = relu(p) * S;
     if (lane == 0) DBR[e] = S;
     float dmean = 0.f;
+    if (gl == w) {  // the prefetched columns (the wave's first graph)
+#pragma unroll
+      for (int k = 0; k < 64; ++k)
+        dmean = fmaf(wpk[k], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dp), k)), dmean);
+    } else {
 #pragma unroll 16
-    for (int k = 0; k < 64; ++k)
-      dmean = fmaf(P[PK_WP + k * 64 + lane], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dp), k)), dmean);
+      for (int k = 0; k < 64; ++k)
+        dmean = fmaf(P[PK_WP + k * 64 + lane], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dp), k)),
+                     dmean);
+    }
     DMEAN[gl * 64 + lane] = dmean / (float)N;
     float dwb = 0.f;
     if (split) {
@@ -941,6 +1002,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   glds_wait();     // Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (staged at the start) are read from here on
   lds_barrier();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
   zero_pad_rows2<NT>(PL, PL1, rows_pad);
+  // the staged adjacency and degrees, first needed by the layers (their loads ran under the readout backward)
+  d3_spread(adjb, adjw);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
   ECO_TS(18);
 
   // ---- update layers in reverse (mpnn.py:114-120) ----
