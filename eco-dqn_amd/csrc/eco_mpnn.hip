@@ -1118,7 +1118,7 @@ int eco::kernel_paths() { return g_kernel_paths.load(std::memory_order_relaxed);
 
 extern "C" int32_t eco_set_kernel_paths(int32_t mask) {
   return g_kernel_paths.exchange(mask & (ECO_PATH_NO_DENSE | ECO_PATH_NO_DL | ECO_PATH_NO_SHARED | ECO_PATH_NO_PAIR |
-                                         ECO_PATH_DENSE2_FWD | 0xFF00));  // 0xFF00: kernel A/B variants
+                                         ECO_PATH_DENSE2_FWD));
 }
 
 struct KCfg {
@@ -1215,7 +1215,7 @@ extern "C" int eco_mpnn_forward_pair(const float* packed_a, const float* packed_
   if (norm_scope == ECO_NORM_PER_CALL && !reuse_maxdeg)
     call_maxdeg_kernel<<<1, 1024, 0, st>>>(*gs, graph_ids, batch, cmax);
   if (paths & ECO_PATH_DENSE2_FWD) return mpnn_forward_dense2_pair_launch(a, b, st);
-  return mpnn_forward_dense3_pair_launch(a, b, st, paths >> 8);
+  return mpnn_forward_dense3_pair_launch(a, b, st);
 }
 
 extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco_graph_set* gs,
@@ -1245,7 +1245,7 @@ extern "C" int eco_mpnn_forward(const float* packed, int32_t n_obs_in, const eco
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
     if (paths & ECO_PATH_DENSE2_FWD) return mpnn_forward_dense2_launch(a, saved != nullptr, st);
-    return mpnn_forward_dense3_launch(a, saved != nullptr, st, paths >> 8);
+    return mpnn_forward_dense3_launch(a, saved != nullptr, st);
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_forward_dl_launch(a, saved != nullptr, workspace, st);
@@ -1307,7 +1307,7 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
   const int paths = kernel_paths();
   if (a.xw == 8 && dense_eligible(gs, a.gpb) && !(paths & ECO_PATH_NO_DENSE)) {
     if (paths & ECO_PATH_DENSE2_FWD) return mpnn_backward_dense2_launch(a, st);
-    return mpnn_backward_dense3_launch(a, st, paths >> 8);
+    return mpnn_backward_dense3_launch(a, st);
   }
   if (a.xw == 8 && dl_eligible(gs, a.gpb) && !(paths & (ECO_PATH_NO_DL | ECO_PATH_NO_DENSE)))
     return mpnn_backward_dl_launch(a, st);

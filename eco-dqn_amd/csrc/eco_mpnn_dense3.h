@@ -43,10 +43,10 @@ __device__ __forceinline__ f16x8 plane_frag(uint32_t b, int kc, int ft) {
   const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(f16x8, raw);
 }
-// aggregation of the wave's two tiles: the pipelined straight-line form when every chunk is live (VAR bit 0)
+// aggregation of the wave's two tiles: the pipelined straight-line form when every chunk is live
 #define AGG3(M, acc, P0, P1, adjw, sc, kc0, kc1, lane)                                        \
   do {                                                                                      \
-    if ((VAR & 1) && kc0 == 0 && kc1 == DN_KC) agg3f<M>(acc, P0, P1, adjw, sc, lane);       \
+    if (kc0 == 0 && kc1 == DN_KC) agg3f<M>(acc, P0, P1, adjw, sc, lane);                    \
     else agg3<M>(acc, P0, P1, adjw, sc, kc0, kc1, lane);                                    \
   } while (0)
 
@@ -275,22 +275,27 @@ __device__ __forceinline__ void zero_acc2(f32x4 (&d)[2][4]) {
 // Staging of the wave's two tiles (d2_stage per tile): row norms, max degrees and spread adjacency words.  One
 // graph per block with a prepared gs.adjbits: per-lane loads; otherwise row info / edge bases / max degrees in LDS
 // and the block bitmask built once (barriers: uniform over the workgroup).
-template <int NT>
+template <int NT, bool PREP>
 __device__ __forceinline__ void d3_stage_raw(const MpnnArgs& a, int blk, int rows_pad, int rows_valid,
                                              const int (&r)[2], const bool (&valid)[2], int s4, int2* RI, int64_t* GB,
                                              int* MD, uint32_t* ADJ, float (&nf)[2], int (&md)[2],
-                                             uint32_t (&adjb)[2][4]) {
+                                             uint32_t (&adjb)[2][4], int gid_v) {
   const int N = a.N;
-  if (a.gpb == 1 && a.gs.adjbits != nullptr) {
-    const int gid = a.gids[blk];  // uniform: scalar load
+  if constexpr (PREP) {  // one graph per block with a prepared gs.adjbits (the launch decides: mpnn_dense3_prep)
+    // gid_v: the block's graph id, loaded by the caller ahead of its other loads.  Every load here is unconditional
+    // (rows clamped, results selected): a load skipped on some path turns each later wait into vmcnt(0), which
+    // serialised the prologue's round trips (graph id, degrees, bitmask, node features)
+    const int gid = uniform_i(gid_v);
     const int mdg = a.gs.max_deg[gid];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int dg = valid[t] ? a.gs.deg[(size_t)gid * N + r[t]] : 1;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (valid[t]) v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + r[t]) * 4 + s4) * 4);
+      // rows past the graph read row 0 (their degree only scales rows that are zeroed; their bitmask words are
+      // masked by d3_spread, after the loads have long landed: a select here became a predicated load)
+      const int rc = valid[t] ? r[t] : 0;
+      const int dl = a.gs.deg[(size_t)gid * N + rc];
+      const uint4 v = *reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + rc) * 4 + s4) * 4);
       adjb[t][0] = v.x; adjb[t][1] = v.y; adjb[t][2] = v.z; adjb[t][3] = v.w;
-      nf[t] = (float)max(dg, 1);
+      nf[t] = (float)max(dl, 1);
       md[t] = mdg;
     }
   } else {
@@ -315,25 +320,18 @@ __device__ __forceinline__ void d3_stage_raw(const MpnnArgs& a, int blk, int row
 }
 // the bitmask words as the spread words of agg3 (the first use of the staged adjacency: placing it late lets the
 // adjacency / degree loads of the prepared-bitmask path run under the forward's phase A)
-__device__ __forceinline__ void d3_spread(const uint32_t (&adjb)[2][4], uint32_t (&adjw)[2][DN_KC]) {
+__device__ __forceinline__ void d3_spread(const uint32_t (&adjb)[2][4], const bool (&valid)[2],
+                                          uint32_t (&adjw)[2][DN_KC]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int kc = 0; kc < DN_KC; ++kc) adjw[t][kc] = adj_spread((adjb[t][kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu);
-}
-template <int NT>
-__device__ __forceinline__ void d3_stage(const MpnnArgs& a, int blk, int rows_pad, int rows_valid, const int (&r)[2],
-                                         const bool (&valid)[2], int s4, int2* RI, int64_t* GB, int* MD,
-                                         uint32_t* ADJ, float (&nf)[2], int (&md)[2],
-                                         uint32_t (&adjw)[2][DN_KC]) {
-  uint32_t adjb[2][4];
-  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, RI, GB, MD, ADJ, nf, md, adjb);
-  d3_spread(adjb, adjw);
+    for (int kc = 0; kc < DN_KC; ++kc)
+      adjw[t][kc] = valid[t] ? adj_spread((adjb[t][kc >> 1] >> (16 * (kc & 1))) & 0xFFFFu) : 0u;
 }
 
 // LDS (ECO_D2_LDS), as mpnn_forward_dense2_kernel.  NNET = 2: the online and the target network on the same graphs
 // and features (a0 then a1), sharing the staging.
-template <bool SAVE, int NNET, int VAR>
+template <bool SAVE, int NNET, bool PREP>
 __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(MpnnArgs a0, MpnnArgs a1) {
   ECO_D2_LDS;
   const MpnnArgs& a = a0;  // the staging reads the graph fields, equal in a0 and a1
@@ -372,18 +370,19 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     r[t] = tl[t] * 16 + c16;
     valid[t] = has[t] && r[t] < rows_valid;
   }
-  // ---- staging: Wf fragments (LDS-DMA); node features, the 8-input Linears' weights and w_a; row norms, max
-  //      degrees and adjacency operands of the lane's two rows ----
+  // ---- staging: the graph id (first: the degree / bitmask loads depend on it); Wf fragments (LDS-DMA); node
+  //      features, the 8-input Linears' weights and w_a; row norms, max degrees and adjacency operands of the
+  //      lane's two rows.  Unconditional loads (rows clamped, results selected): see d3_stage_raw ----
+  const int gid_v = a.gids[min(blk * a.gpb, a.B - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // issued before the loads below (waiting for it then leaves them in flight)
   glds_frags<NW>(WB0, PH + FH_WF, 16, w, lane);
   float xk0[2], xk1[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    xk0[t] = 0.f;
-    xk1[t] = 0.f;
-    if (valid[t]) {
-      xk0[t] = a.x[(R0 + r[t]) * 8 + s4];
-      xk1[t] = a.x[(R0 + r[t]) * 8 + 4 + s4];
-    }
+    const size_t row = R0 + (valid[t] ? r[t] : 0);
+    const float x0 = a.x[row * 8 + s4], x1 = a.x[row * 8 + 4 + s4];
+    xk0[t] = valid[t] ? x0 : 0.f;
+    xk1[t] = valid[t] ? x1 : 0.f;
   }
   float wx8[8], w08[8];
   lin8_load(P + PK_WX, lane, wx8);
@@ -394,7 +393,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   float nf[2];
   int md_graph[2];
   uint32_t adjb[2][4], adjw[2][DN_KC];
-  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, r, valid, s4, sRI, sGB, sMD, ADJ, nf, md_graph, adjb);
+  d3_stage_raw<NT, PREP>(a, blk, rows_pad, rows_valid, r, valid, s4, sRI, sGB, sMD, ADJ, nf, md_graph, adjb, gid_v);
   ECO_TS(1);
   float rnf[2];
   // aggregation chunks of the wave's rows (the union of its two tiles' ranges)
@@ -445,7 +444,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   lds_barrier();
   ECO_TS(2);
   if (first) {  // the staged adjacency and degrees, first needed here
-    d3_spread(adjb, adjw);
+    d3_spread(adjb, valid, adjw);
 #pragma unroll
     for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
   }
@@ -588,12 +587,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         kx[t] = node_exp2(agg[t], ereg[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if constexpr (VAR & 2) {
         lin128_2t<D3_LIN_SPLIT_AHEAD && !SAVE && NNET == 1>(d, ereg[0], ereg[1], WM + FH_HALF, agg[0], agg[1], WM, sf, lane);
-      } else {
-        mm_fh_2t(d, ereg[0], ereg[1], sf, WM + FH_HALF, lane);
-        mm_fh_2t(d, agg[0], agg[1], sf, WM, lane);
-      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         unscale(d[t], kx[t] + kwm);
@@ -623,12 +617,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         kx[t] = node_exp2(hreg[t], mrel[t]);
         sf[t] = exp2i(kx[t]);
       }
-      if constexpr (VAR & 2) {
         lin128_2t<D3_LIN_SPLIT_AHEAD && !SAVE && NNET == 1>(hn, hreg[0], hreg[1], WU, mrel[0], mrel[1], WU + FH_HALF, sf, lane);
-      } else {
-        mm_fh_2t(hn, hreg[0], hreg[1], sf, WU, lane);
-        mm_fh_2t(hn, mrel[0], mrel[1], sf, WU + FH_HALF, lane);
-      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         unscale(hn[t], kx[t] + kwu);
@@ -767,37 +756,24 @@ static int dense3_check(const MpnnArgs& a) {
   return ECO_OK;
 }
 
-template <int VAR>
-static int mpnn_forward_dense3_launch_v(const MpnnArgs& a, bool save, hipStream_t st) {
+// the staging path of the launch (one graph per block with a prepared gs.adjbits: per-lane loads) as a template
+// argument: a run-time branch merged the two paths' registers and turned every staging wait into vmcnt(0)
+inline bool mpnn_dense3_prep(const MpnnArgs& a) { return a.gpb == 1 && a.gs.adjbits != nullptr; }
+static int mpnn_forward_dense3_launch(const MpnnArgs& a, bool save, hipStream_t st) {
+  if (const int rc = dense3_check(a)) return rc;
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  if (save) mpnn_forward_dense3_kernel<true, 1, VAR><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
-  else mpnn_forward_dense3_kernel<false, 1, VAR><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  const bool prep = mpnn_dense3_prep(a);
+  if (save && prep) mpnn_forward_dense3_kernel<true, 1, true><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  else if (save) mpnn_forward_dense3_kernel<true, 1, false><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  else if (prep) mpnn_forward_dense3_kernel<false, 1, true><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
+  else mpnn_forward_dense3_kernel<false, 1, false><<<blocks, 64 * D3_NW, 0, st>>>(a, a);
   return check_launch("mpnn_forward_dense3");
 }
-// var: the kernel-path bits 8-9 (eco_set_kernel_paths), A/B of the schedules -- bit 8 set: the aggregation without
-// the software pipeline (agg3), bit 9 set: the Linears without it (mm_fh_2t); default both pipelined (measured
-// fastest).  All four are bitwise equal.
-__host__ inline int dense3_variant(int var) { return (var & 3) ^ 3; }
-static int mpnn_forward_dense3_launch(const MpnnArgs& a, bool save, hipStream_t st, int var) {
+static int mpnn_forward_dense3_pair_launch(const MpnnArgs& a, const MpnnArgs& b, hipStream_t st) {
   if (const int rc = dense3_check(a)) return rc;
-  var = dense3_variant(var);
-  switch (var & 3) {
-    case 1: return mpnn_forward_dense3_launch_v<1>(a, save, st);
-    case 2: return mpnn_forward_dense3_launch_v<2>(a, save, st);
-    case 3: return mpnn_forward_dense3_launch_v<3>(a, save, st);
-    default: return mpnn_forward_dense3_launch_v<0>(a, save, st);
-  }
-}
-static int mpnn_forward_dense3_pair_launch(const MpnnArgs& a, const MpnnArgs& b, hipStream_t st, int var) {
-  if (const int rc = dense3_check(a)) return rc;
-  var = dense3_variant(var);
   if (a.gpb != 1) return fail(ECO_ERR_ARG, "paired dense forward: one graph per block only");
-  switch (var & 3) {
-    case 1: mpnn_forward_dense3_kernel<false, 2, 1><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
-    case 2: mpnn_forward_dense3_kernel<false, 2, 2><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
-    case 3: mpnn_forward_dense3_kernel<false, 2, 3><<<a.B, 64 * D3_NW, 0, st>>>(a, b); break;
-    default: mpnn_forward_dense3_kernel<false, 2, 0><<<a.B, 64 * D3_NW, 0, st>>>(a, b);
-  }
+  if (mpnn_dense3_prep(a)) mpnn_forward_dense3_kernel<false, 2, true><<<a.B, 64 * D3_NW, 0, st>>>(a, b);
+  else mpnn_forward_dense3_kernel<false, 2, false><<<a.B, 64 * D3_NW, 0, st>>>(a, b);
   return check_launch("mpnn_forward_dense3_pair");
 }
 
@@ -842,7 +818,7 @@ __device__ __forceinline__ void mm_fh2_2t(f32x4 (&acc0)[2][4], f32x4 (&acc1)[2][
 // strided node sums run over 16 virtual waves, dw_a's per-tile partials are summed in tile order over 16 slots --
 // so the gradients are bitwise those of mpnn_backward_dense2_kernel (tests/test_dense_gpu.py).
 // LDS (ECO_D2_LDS): sPL 2 planes (readout scratch first) | sW0, sW1, sW2 | TE | RI | GB
-template <int VAR>
+template <bool PREP>
 __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(MpnnArgs a) {
   ECO_D2_LDS;
   ECO_TS(16);
@@ -886,7 +862,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   auto WMT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE; };                // Wm^T: dagg, de halves
   KwLoad kw(P);  // the matrix scales: loaded here, made wave-uniform where they are used
 
-  // ---- staging: Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (LDS-DMA), row info, edge bases ----
+  // ---- staging: the graph id (see the forward), Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (LDS-DMA), row info,
+  //      edge bases ----
+  const int gid_v = a.gids[min(blk * a.gpb, a.B - 1)];
+  __builtin_amdgcn_sched_barrier(0);
   glds_frags<NW>(WB0, WUT(2), 32, w, lane);
   glds_frags<NW>(WB1, WMT(2), 32, w, lane);
   glds_frags<NW>(WB2, WUT(1), 32, w, lane);
@@ -904,7 +883,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   float nf[2], rnf[2];
   int md_unused[2];
   uint32_t adjb[2][4], adjw[2][DN_KC];
-  d3_stage_raw<NT>(a, blk, rows_pad, rows_valid, rw, valid, s4, sRI, sGB, sMD, ADJ, nf, md_unused, adjb);
+  d3_stage_raw<NT, PREP>(a, blk, rows_pad, rows_valid, rw, valid, s4, sRI, sGB, sMD, ADJ, nf, md_unused, adjb, gid_v);
   const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
@@ -1003,7 +982,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   lds_barrier();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
   zero_pad_rows2<NT>(PL, PL1, rows_pad);
   // the staged adjacency and degrees, first needed by the layers (their loads ran under the readout backward)
-  d3_spread(adjb, adjw);
+  d3_spread(adjb, valid, adjw);
 #pragma unroll
   for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
   ECO_TS(18);
@@ -1239,12 +1218,11 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   ECO_TS(23);
 }
 
-static int mpnn_backward_dense3_launch(const MpnnArgs& a, hipStream_t st, int var) {
+static int mpnn_backward_dense3_launch(const MpnnArgs& a, hipStream_t st) {
   if (const int rc = dense3_check(a)) return rc;
-  var = dense3_variant(var);
   const int blocks = (a.B + a.gpb - 1) / a.gpb;
-  if (var & 1) mpnn_backward_dense3_kernel<1><<<blocks, 64 * D3_NW, 0, st>>>(a);
-  else mpnn_backward_dense3_kernel<0><<<blocks, 64 * D3_NW, 0, st>>>(a);
+  if (mpnn_dense3_prep(a)) mpnn_backward_dense3_kernel<true><<<blocks, 64 * D3_NW, 0, st>>>(a);
+  else mpnn_backward_dense3_kernel<false><<<blocks, 64 * D3_NW, 0, st>>>(a);
   return check_launch("mpnn_backward_dense3");
 }
 

@@ -41,8 +41,8 @@ def test_set_kernel_paths_returns_previous_and_masks_unknown_bits():
     """eco_set_kernel_paths is host-only: the policy word the MPNN dispatcher reads (no GPU needed)."""
     from eco_hip import _lib
     prev = _lib.lib.eco_set_kernel_paths(0x7FFFFFFF)
-    # documented bits (NO_DENSE .. DENSE2_FWD) and the dense3 schedule bits 8-15; nothing else survives
-    assert _lib.lib.eco_set_kernel_paths(prev) == 0x1F | 0xFF00
+    # the documented bits (NO_DENSE .. DENSE2_FWD); nothing else survives
+    assert _lib.lib.eco_set_kernel_paths(prev) == 0x1F
     with _lib.kernel_paths(_lib.ECO_PATH_NO_PAIR):
         assert _lib.lib.eco_set_kernel_paths(_lib.ECO_PATH_NO_PAIR) == _lib.ECO_PATH_NO_PAIR
     assert _lib.lib.eco_set_kernel_paths(prev) == prev
