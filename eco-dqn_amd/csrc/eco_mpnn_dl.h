@@ -187,35 +187,40 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_forward_dl_kernel(MpnnArgs
   int* TE = sTE;
 
   // ---- staging: Wf (LDS-DMA); per tile the row norm, adjacency operand and node features ----
+  const int gid = a.gids[blk];  // first: the staging loads depend on it (waiting for it leaves the DMA in flight)
+  __builtin_amdgcn_sched_barrier(0);
   glds_frags<NW>(sW2, PH + FH_WF, 16, w, lane);
-  const int gid = a.gids[blk];
   const int md_graph = a.gs.max_deg[gid];
   int rI[MT];
   bool vI[MT];
   float nf[MT], rnf[MT], xk0[MT], xk1[MT];
   uint32_t adj[MT][DL_AW];
+  // unconditional loads (rows past the graph read row 0; degrees and bitmask words are masked below, after the
+  // loop): a load skipped on some path made each tile's staging wait for the previous tile's (vmcnt(4) per tile)
+  int dgr[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     rI[i] = (w + NW * i) * 16 + c16;
     vI[i] = i < ntw && rI[i] < N;
-    int dg = 1;
-    uint4 a0 = make_uint4(0u, 0u, 0u, 0u), a1 = a0;
-    xk0[i] = xk1[i] = 0.f;
-    if (vI[i]) {
-      dg = a.gs.deg[(size_t)gid * N + rI[i]];
-      const uint4* ap = reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + rI[i]) * 4 + s4) * DL_AW);
-      a0 = ap[0];
-      a1 = ap[1];
-      xk0[i] = a.x[(R0 + rI[i]) * 8 + s4];
-      xk1[i] = a.x[(R0 + rI[i]) * 8 + 4 + s4];
-    }
-    nf[i] = (float)max(dg, 1);
-    rnf[i] = 1.f / nf[i];
+    const int rc = vI[i] ? rI[i] : 0;
+    dgr[i] = a.gs.deg[(size_t)gid * N + rc];
+    const uint4* ap = reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + rc) * 4 + s4) * DL_AW);
+    const uint4 a0 = ap[0], a1 = ap[1];
+    const float x0 = a.x[(R0 + rc) * 8 + s4], x1 = a.x[(R0 + rc) * 8 + 4 + s4];
+    xk0[i] = vI[i] ? x0 : 0.f;
+    xk1[i] = vI[i] ? x1 : 0.f;
     adj[i][0] = a0.x; adj[i][1] = a0.y; adj[i][2] = a0.z; adj[i][3] = a0.w;
     adj[i][4] = a1.x; adj[i][5] = a1.y; adj[i][6] = a1.z; adj[i][7] = a1.w;
   }
   dl_zero_pad<NT>(PL0, PL1, rows_pad);
   dl_zero_pad<NT>(sW0, sW1, rows_pad);  // V planes
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    nf[i] = vI[i] ? (float)max(dgr[i], 1) : 1.f;
+    rnf[i] = 1.f / nf[i];
+#pragma unroll
+    for (int k = 0; k < DL_AW; ++k) adj[i][k] = vI[i] ? adj[i][k] : 0u;
+  }
   ECO_TS(1);
 
   // ---- phases A + B: edge embedding (mpnn.py:89-104): (A+ . relu(Z + w_a) + A- . relu(Z - w_a)) / norm, per
@@ -566,31 +571,27 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_backward_dl_kernel(MpnnArg
   auto WMT = [&](int l) { return PH + FHT_LAYER + l * FH_LAYER_STRIDE; };
 
   // ---- staging: Wu^T / Wm^T of layer 2, Wf^T (LDS-DMA); per tile norm, adjacency operand, ReLU masks ----
+  const int gid = a.gids[blk];  // first (see the forward)
+  __builtin_amdgcn_sched_barrier(0);
   glds_frags<NW>(sW0, WUT(2), 32, w, lane);
   glds_frags<NW>(sW1, WMT(2), 32, w, lane);
   glds_frags<NW>(sW2, PH + FHT_WF, 16, w, lane);
-  const int gid = a.gids[blk];
   const uint16_t* Msk = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
   int rI[MT];
   bool vI[MT];
   float rnf[MT];
   uint32_t adj[MT][DL_AW];
   uint4 rmask[MT];
+  int dgr[MT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+  for (int i = 0; i < MT; ++i) {  // unconditional loads, masked after the loop (see the forward)
     rI[i] = (w + NW * i) * 16 + c16;
     vI[i] = i < ntw && rI[i] < N;
-    int dg = 1;
-    uint4 a0 = make_uint4(0u, 0u, 0u, 0u), a1 = a0;
-    rmask[i] = a0;
-    if (vI[i]) {
-      dg = a.gs.deg[(size_t)gid * N + rI[i]];
-      const uint4* ap = reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + rI[i]) * 4 + s4) * DL_AW);
-      a0 = ap[0];
-      a1 = ap[1];
-      rmask[i] = *reinterpret_cast<const uint4*>(Msk + ((R0 + rI[i]) * 4 + s4) * SM_TENSORS);
-    }
-    rnf[i] = 1.f / (float)max(dg, 1);
+    const int rc = vI[i] ? rI[i] : 0;
+    dgr[i] = a.gs.deg[(size_t)gid * N + rc];
+    const uint4* ap = reinterpret_cast<const uint4*>(a.gs.adjbits + (((size_t)gid * N + rc) * 4 + s4) * DL_AW);
+    const uint4 a0 = ap[0], a1 = ap[1];
+    rmask[i] = *reinterpret_cast<const uint4*>(Msk + ((R0 + rc) * 4 + s4) * SM_TENSORS);
     adj[i][0] = a0.x; adj[i][1] = a0.y; adj[i][2] = a0.z; adj[i][3] = a0.w;
     adj[i][4] = a1.x; adj[i][5] = a1.y; adj[i][6] = a1.z; adj[i][7] = a1.w;
   }
@@ -647,6 +648,14 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_backward_dl_kernel(MpnnArg
   }
   glds_wait();     // Wu^T / Wm^T of layer 2 and Wf^T
   lds_barrier();  // readout scratch dead
+  // the staged degrees, bitmask words and ReLU masks of rows past the graph (loaded from row 0), first needed below
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    rnf[i] = vI[i] ? 1.f / (float)max(dgr[i], 1) : 1.f;
+    if (!vI[i]) rmask[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < DL_AW; ++k) adj[i][k] = vI[i] ? adj[i][k] : 0u;
+  }
   dl_zero_pad<NT>(PL0, PL1, rows_pad);
   ECO_TS(18);
 
