@@ -502,6 +502,36 @@ def test_regenerate_graphs_with_replay_longer_than_an_episode_batch():
     assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()
 
 
+def test_evaluation_on_the_regenerated_training_store_is_synchronous(tmp_path):
+    """with regenerate_graphs and test_envs=None the test env reads the training slot store,
+    which the main stream regenerates while training goes on; learn() must not overlap such an evaluation (no event
+    orders the regeneration after the side stream).  Overlap on and off give the same scores, solutions, losses and
+    `_best` file, and the overlap-on run evaluated synchronously."""
+    from eco_hip.graphs import GraphStore, edge_cap
+    from eco_hip.agents.dqn.dqn import graph_slots_needed
+    from eco_hip.agents.dqn.utils import TestMetric
+    n, B = 20, 64
+    T = 2 * n
+    C = B * T
+    out = []
+    for overlap in (False, True):
+        st = GraphStore.slots(graph_slots_needed(B, T, C), n, edge_cap("ER", n, 0.15))
+        d = tmp_path / str(overlap)
+        d.mkdir()
+        agent = _dqn_for(st, n, B=B, replay_buffer_size=C, replay_start_size=2 * B, train_minibatch=64,
+                         regenerate_graphs=("ER", 0.15), evaluate=True, test_envs=None, test_episodes=8,
+                         test_frequency=B * 10, test_metric=TestMetric.BEST, save_network_frequency=B * 1000,
+                         network_save_path=str(d / "network.pth"), test_save_path=None, overlap_evaluation=overlap)
+        assert not agent._overlap_ok(agent._test_env())
+        losses = agent.learn(timesteps=B * T * 2)
+        best = torch.load(d / "network_best.pth", map_location="cpu", weights_only=True)
+        out.append((agent.test_scores, agent.test_solutions, losses, best, agent._eval_net is not None))
+    (s0, o0, l0, b0, e0), (s1, o1, l1, b1, e1) = out
+    assert not e0 and not e1  # neither run overlapped
+    assert len(s0) == B * T * 2 // (B * 10) and s0 == s1 and o0 == o1 and l0 == l1
+    assert all(torch.equal(b0[k], b1[k]) for k in b0)
+
+
 def test_learn_with_staggered_dones_resets_only_finished_episodes():
     """with Stopping.EARLY (spinsystem.py:541-556, done after 15 steps without a new best)
     episodes finish at different steps, so learn() takes the partial-reset path of iteration() (dqn.py:306-327
