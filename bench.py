@@ -197,8 +197,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r04", "final", "train", "pmc_hbm.json")
-PMC_SQ = os.path.join(REPO, "profiles", "r04", "final", "train", "pmc_sq_dense.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r05", "final", "train", "pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r05", "final", "train", "pmc_sq_dense.json")
 PMC_PAIRED = True  # the committed train PMC pass ran the paired s' forward (eco_mpnn_forward_pair)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
 
@@ -225,7 +225,7 @@ def mfma_roofline(achieved_tflops, kernel):
             "frac_vs_f32_mfma_peak": achieved_tflops / FP32_MFMA_PEAK_TFLOPS}
 # kernel names of the dense path, newest first (the PMC summaries of earlier rounds carry the older ones)
 FWD_NAMES = ("mpnn_forward_dense3_kernel", "mpnn_forward_dense2_kernel", "mpnn_forward_dense_kernel")
-BWD_NAMES = ("mpnn_backward_dense2_kernel", "mpnn_backward_dense_kernel")
+BWD_NAMES = ("mpnn_backward_dense3_kernel", "mpnn_backward_dense2_kernel", "mpnn_backward_dense_kernel")
 WGRAD_NAMES = ("wgrad_fh_kernel", "wgrad_bf3_kernel", "wgrad_kernel")
 
 
@@ -235,8 +235,7 @@ PMC_GSET = os.path.join(REPO, "profiles", "r04", "final", "gset_pmc", "pmc_hbm.j
 
 
 def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
-    """MFMA evidence of the dominant kernel from the committed SQ PMC pass (profiles/r03/train/
-    pmc_sq_dense.json, ER-200 M=2048): MFMA-busy fraction (launch mix of the train loop: inference forwards
+    """MFMA evidence of the dominant kernel from the committed SQ PMC pass (PMC_SQ, ER-200 M=2048): MFMA-busy fraction (launch mix of the train loop: inference forwards
     of act and of s', training forwards with saved activations) and the ratio of ISSUED f16 MFMA FLOPs
     (fp16x2 splits, dense N^2 aggregations) to the algorithmic FLOPs, so the issued rate can be priced
     against the f16 peak beside the f32-algorithmic fraction."""
@@ -245,8 +244,8 @@ def pmc_mfma(dom, B, M, n, graph, flops_per_graph):
     try:
         with open(PMC_SQ) as f:
             k = json.load(f)["kernels"]
-        inf = _first(k, [n + t for n in FWD_NAMES for t in ("<false, 1>", "<false>")])
-        trn = _first(k, [n + t for n in FWD_NAMES for t in ("<true, 1>", "<true>")])
+        inf = _first(k, [n + t for n in FWD_NAMES for t in ("<false, 1, true>", "<false, 1>", "<false>")])
+        trn = _first(k, [n + t for n in FWD_NAMES for t in ("<true, 1, true>", "<true, 1>", "<true>")])
     except (OSError, ValueError, KeyError):
         return None
     n_inf, n_trn = 1 + 2 * (B * 2 // M), B * 2 // M  # act + online/target(s') per grad step (their work, paired
@@ -508,7 +507,8 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     episodes push B per vector step, so a ring of one episode's worth holds every time step of the episodes
     (the reference's 15,000 transitions span ~19 whole ER-200 episodes); B x 16 (round 3) held only the last 16
     steps and measured 0.935 of the pretrained network's single-attempt cut against 0.974-0.991 with B x T
-    (profiles/r04/quality/).  tests/test_training_quality_er200_gpu.py trains this exact agent.
+    (profiles/r04/quality/; round 5: profiles/r05/quality/).  tests/test_training_quality_er200_gpu.py trains this
+    exact agent.
     regenerate (default): a fresh ER / BA graph for every episode, as the reference's env.reset() draws one
     (src/agents/dqn/dqn.py:306-327 -> src/envs/spinsystem.py:191-196 -> src/envs/utils.py:192-236): the store holds
     graph_slots_needed(B, T, ring) slots (two batches of B at one episode's ring), generated on the device, and
