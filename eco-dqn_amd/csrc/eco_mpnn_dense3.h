@@ -22,6 +22,16 @@
 namespace eco {
 
 constexpr int D3_NW = 8;  // waves per workgroup
+// Priority checkpoints inside a forward layer (A/B: D3_SETPRIO): the priority drops at each checkpoint a wave
+// passes and is restored after each barrier, so of the two waves of a SIMD the one behind is issued first and they
+// reach the barrier together (the arbiter's oldest-first choice otherwise lets one run ahead and wait)
+#ifndef D3_SETPRIO
+#define D3_SETPRIO 1
+#endif
+#define D3_PRIO(k)                                     \
+  do {                                                 \
+    if (D3_SETPRIO) __builtin_amdgcn_s_setprio(k);     \
+  } while (0)
 #ifndef D3_LIN_SPLIT_AHEAD
 #define D3_LIN_SPLIT_AHEAD 1  // A/B: the inference forward's Linears split one step ahead
 #endif
@@ -442,6 +452,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   glds_wait();  // Wf fragments
   ECO_TS(15);
   lds_barrier();
+  D3_PRIO(3);
   ECO_TS(2);
   if (first) {  // the staged adjacency and degrees, first needed here
     d3_spread(adjb, valid, adjw);
@@ -459,6 +470,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     zero_acc2(ev);
     AGG3(1, ea, PL, PL1, adjw, su, kc0, kc1, lane);
     AGG3(2, ev, WB1, WB2, adjw, sv, kc0, kc1, lane);
+    D3_PRIO(2);
     const int maxdeg_call = a.norm_scope == ECO_NORM_PER_CALL ? *a.call_maxdeg : 0;
     float4 acc[2][4];
     float sfx[2];
@@ -502,7 +514,9 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_E, pos_mask(ereg[t]));
     }
   }
+  D3_PRIO(1);
   lds_barrier();  // every wave is done with the U / V planes and with Wf
+  D3_PRIO(3);
   ECO_TS(3);
   // layer weights: Wm0 -> WB1, Wu0 -> WB2, Wm1 -> WB0 (landed by layer 0's first barrier)
   glds_frags<NW>(WB1, PH + FH_LAYER, 32, w, lane);
@@ -532,6 +546,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       for (int c = 0; c < 4; ++c) hreg[t][c] = zero4();
   }
   lds_barrier();
+  D3_PRIO(3);
   ECO_TS(4);
 
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120) ----
@@ -562,9 +577,11 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       for (int c = 0; c < 4; ++c)
         agg[t][c] = make_float4(ag[t][c][0] * sc, ag[t][c][1] * sc, ag[t][c][2] * sc, ag[t][c][3] * sc);
     }
+    D3_PRIO(2);
     if (layer == 0) ECO_TS(10);
     glds_wait();
     lds_barrier();  // B1: planes read by every wave; this layer's weights landed
+    D3_PRIO(3);
     if (layer == 0) ECO_TS(11);
     if (SAVE) {  // after the wait: stores count in vmcnt with the weight DMA
 #pragma unroll
@@ -605,6 +622,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         store_mask(a, RT, R0 + r[t], s4, SM_M0 + layer, pos_mask(mrel[t]));
       }
     }
+    D3_PRIO(2);
     if (layer == 0) ECO_TS(12);
     // h' = relu(Wu . [h, m])
     {
@@ -630,14 +648,17 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_H1 + layer, pos_mask(hreg[t]));
       }
     }
+    D3_PRIO(1);
     if (layer == 0) ECO_TS(13);
     if (layer < 2) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
     }
+    D3_PRIO(0);
     if (layer == 0) ECO_TS(14);
     lds_barrier();  // B2: planes of h_{layer+1} complete; this layer's weight buffers free
+    D3_PRIO(3);
     ECO_TS(5 + layer);
   }
   if (next)  // the next network's Wf into the free buffer, landing while this readout runs
@@ -1031,9 +1052,11 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         for (int c = 0; c < 4; ++c) dum[t][c] = masked(dmm[t][c], mmask, c);
       }
     }
+    D3_PRIO(2);
     if (layer == 1) ECO_TS(24);
     glds_wait();
     lds_barrier();  // B0: Wm^T landed
+    D3_PRIO(3);
     if (layer == 1) ECO_TS(25);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1058,6 +1081,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         sf[t] = exp2i(kx[t]);
       }
       mm_fh2_2t(dg, dd, dum[0], dum[1], sf, WM, WM + FH_HALF, lane);
+      D3_PRIO(2);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int km = kx[t] + kwm;
@@ -1074,8 +1098,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
         if (has[t]) tile_planes(PL, PL1, TE, tl[t], rw[t], s4, g, lane);
       }
     }
+    D3_PRIO(1);
     if (layer == 1) ECO_TS(26);
     lds_barrier();  // B1: G planes complete; every wave is past both Linears: this layer's weight buffers free
+    D3_PRIO(3);
     if (layer == 2) {
       glds_frags<NW>(WB0, WMT(1), 32, w, lane);
       glds_frags<NW>(WB1, WUT(0), 32, w, lane);
@@ -1104,8 +1130,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
           dh[t][c] = valid[t] ? make_float4(t4[0], t4[1], t4[2], t4[3]) : zero4();
         }
     }
+    D3_PRIO(2);
     if (layer == 1) ECO_TS(28);
     lds_barrier();  // B2: planes read
+    D3_PRIO(3);
     ECO_TS(21 - layer);
   }
 
