@@ -793,6 +793,9 @@ def inference_bench(args, world, rank, local, dev, dist):
             "roofline": dict(mfma_roofline(fl / (fwd_ms * 1e-3) / 1e12, forward_kernel_name(n, kind, ngraphs)),
                              traffic=None, avg_launch_ms=fwd_ms, flops_per_launch=fl),
             "best_cut_after_steps": best_cut,
+            "best_cut_note": ("random-init network after the timed steps (a throughput by-product); the full search "
+                              "with the pretrained network: tools/gset_search.py, profiles/r05/gset_search_1024.json"
+                              if args.workload == "gset" else "random-init network after the timed steps"),
             "process_group": pg,
         }
         if args.workload == "gset":

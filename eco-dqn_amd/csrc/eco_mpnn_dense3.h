@@ -909,11 +909,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
   const uint16_t* Msk = reinterpret_cast<const uint16_t*>(sv + sv_mask_offset_floats(RT, a.B));
-  uint4 rmask[2];
+  uint4 rmask[2];  // unconditional loads (row clamped), masked after the readout (see d3_stage_raw)
 #pragma unroll
   for (int t = 0; t < 2; ++t)
-    rmask[t] = valid[t] ? *reinterpret_cast<const uint4*>(Msk + ((R0 + rw[t]) * 4 + s4) * SM_TENSORS)
-                        : make_uint4(0u, 0u, 0u, 0u);
+    rmask[t] = *reinterpret_cast<const uint4*>(Msk + ((R0 + min(rw[t], rows_valid - 1)) * 4 + s4) * SM_TENSORS);
   ECO_TS(17);
 
   // ---- readout backward (mpnn.py:143-159), scratch in the plane region ----
@@ -1005,7 +1004,10 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   // the staged adjacency and degrees, first needed by the layers (their loads ran under the readout backward)
   d3_spread(adjb, valid, adjw);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) rnf[t] = 1.f / nf[t];
+  for (int t = 0; t < 2; ++t) {
+    rnf[t] = 1.f / nf[t];
+    if (!valid[t]) rmask[t] = make_uint4(0u, 0u, 0u, 0u);
+  }
   ECO_TS(18);
 
   // ---- update layers in reverse (mpnn.py:114-120) ----
@@ -1180,15 +1182,12 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   ECO_TS(22);
   // dz_j = [z_j + w_a > 0] (A+ . G)_j + [z_j - w_a > 0] (A- . G)_j;  dw_a = sum_j of the same with signs
   {
-    float xk0[2], xk1[2];  // inputs of Z, loaded ahead of the aggregations
+    float xk0[2], xk1[2];  // inputs of Z, loaded ahead of the aggregations (row clamped: invalid rows masked below)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      xk0[t] = 0.f;
-      xk1[t] = 0.f;
-      if (valid[t]) {
-        xk0[t] = a.x[(R0 + rw[t]) * 8 + s4];
-        xk1[t] = a.x[(R0 + rw[t]) * 8 + 4 + s4];
-      }
+      const size_t row = R0 + min(rw[t], rows_valid - 1);
+      xk0[t] = a.x[row * 8 + s4];
+      xk1[t] = a.x[row * 8 + 4 + s4];
     }
     float wx8[8];
     lin8_load(P + PK_WX, lane, wx8);

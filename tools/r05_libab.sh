@@ -18,6 +18,6 @@ for rep in 1 2; do
     lib="$ROOT/eco-dqn_amd/eco_hip/libecohip.so"; [ "$v" != product ] && lib="$ROOT/eco-dqn_amd/eco_hip/libecohip_$v.so"
     ECO_HIP_LIB="$lib" timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline ${4:-} \
       > "$OUT/bench_${v}_r$rep.json" 2> "$OUT/bench_${v}_r$rep.err" || { tail -5 "$OUT/bench_${v}_r$rep.err"; exit 5; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], round(d['value']), round(d['ms_per_step'],3), r.get('kernel'), round(r.get('avg_launch_ms',0) or 0,4), round(r['frac'],4))" "$OUT/bench_${v}_r$rep.json" "$v r$rep"
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], round(d['value']), round(d['ms_per_step'],3), r.get('kernel'), round(r.get('avg_launch_ms',0) or 0,4), round(r['frac'],4), {k: round(v,3) for k,v in d.get('kernels_ms_per_step',{}).items()})" "$OUT/bench_${v}_r$rep.json" "$v r$rep"
   done
 done
