@@ -498,12 +498,15 @@ def process_group_info(world, per_rank_s, steps, local, device):
             "ms_per_step_min": min(ms), "ms_per_step_max": max(ms)}
 
 
+TARGET_SYNC_GRAD_STEPS = 16
+
+
 def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=1.0,
                       n_graphs=None, regenerate=True):
     """The benched configs[2] / configs[3] agent: B episodes on a pool of B seeded graphs (one per episode),
     experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377) batched, with the large-batch recipe of
-    tests/test_training_quality_gpu.py (target sync every update_target_frequency / update_frequency gradient
-    steps, lr 1e-4 x sqrt(M / 64)) and a replay ring of `replay_episodes` x B x T transitions: the B lockstep
+    tests/test_training_quality_gpu.py (lr 1e-4 x sqrt(M / 64); target sync every TARGET_SYNC_GRAD_STEPS gradient
+    steps) and a replay ring of `replay_episodes` x B x T transitions: the B lockstep
     episodes push B per vector step, so a ring of one episode's worth holds every time step of the episodes
     (the reference's 15,000 transitions span ~19 whole ER-200 episodes); B x 16 (round 3) held only the last 16
     steps and measured 0.935 of the pretrained network's single-attempt cut against 0.974-0.991 with B x T
@@ -538,6 +541,11 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
                 initial_exploration_rate=1, final_exploration_rate=0.05, final_exploration_step=800000,
                 adam_epsilon=1e-8, seed=seed, target_sync="grad_steps",
                 regenerate_graphs=(graph, gparam) if regenerate else None)
+    # target sync every TARGET_SYNC_GRAD_STEPS gradient steps (16,384 env-steps) instead of the reference's
+    # update_target_frequency / update_frequency = 125: round-5 sweeps (profiles/r05/quality/) measured ER-200
+    # single-attempt 0.989 (nine seeds) against 0.983 at 125, BA-200 1.010 against 1.012; one copy of the parameter
+    # vector, no throughput cost
+    agent.target_sync_grad_steps = TARGET_SYNC_GRAD_STEPS
     return agent, store, env, lr
 
 
