@@ -703,10 +703,12 @@ class DQN:
         acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
         sub = acts[:k]
         act_cfg.counter = 0
+        scope = _lib.ECO_NORM_PER_CALL  # the batch obs_x[:k] never changes: its max degree once, then reused
         for _ in range(env.max_steps):
-            net.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=_lib.ECO_NORM_PER_CALL,
+            net.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=scope,
                                act=act_cfg, actions_out=sub)
             _, rew, _ = env.step(acts)
+            scope = _lib.ECO_NORM_PER_CALL_REUSE
             cum += rew
         st = env.read()  # device scalars; read by _eval_one_fill_finish
         return {"env": env, "k": k, "cum": cum, "st": st, "metric": self.test_metric}

@@ -137,10 +137,11 @@ def test_network(network, env_args, graphs_test, device=None, step_factor=1, bat
             act = _lib.ActConfig(0.0, int(reversible), allowed, 0, 0)
             torch.cuda.synchronize(dev)
             t0 = time.time()
+            scope = _lib.ECO_NORM_PER_CALL  # same batch every step: the call's max degree once, then reused
             for _ in range(n_steps):
-                network.forward_graphs(env.obs_x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL, act=act,
-                                       actions_out=acts)
+                network.forward_graphs(env.obs_x, store, gids, norm_scope=scope, act=act, actions_out=acts)
                 env.step(acts)
+                scope = _lib.ECO_NORM_PER_CALL_REUSE
             st = env.read(best_spins=True)
             torch.cuda.synchronize(dev)
             t_total += time.time() - t0
