@@ -700,6 +700,7 @@ class DQN:
         env._eval_next_graph = (env._eval_next_graph + k) % n_graphs
         env.reset(graph_ids=gids, mask=mask, seed=self.eval_seed)
         cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
+        keep_cum = self.test_metric == TestMetric.CUMULATIVE_REWARD
         acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
         sub = acts[:k]
         act_cfg.counter = 0
@@ -709,7 +710,8 @@ class DQN:
                                act=act_cfg, actions_out=sub)
             _, rew, _ = env.step(acts)
             scope = _lib.ECO_NORM_PER_CALL_REUSE
-            cum += rew
+            if keep_cum:  # only the cumulative-reward metric reads it: one elementwise launch fewer per step
+                cum += rew
         st = env.read()  # device scalars; read by _eval_one_fill_finish
         return {"env": env, "k": k, "cum": cum, "st": st, "metric": self.test_metric}
 
