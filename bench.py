@@ -336,41 +336,52 @@ def envstep_rate(dev, B, n, steps=200, warmup=5, seed=1234, store=None):
     return B / (ms * 1e-3), ms
 
 
-def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000, graph="ER", gparam=0.15):
-    """What the timed vector steps never contain (T = 2N steps per episode, 20 timed steps): the full reset of
-    all B episodes at an episode boundary (fresh spins, compact-replay snapshot; dqn.py:306-327), and one
-    evaluate_agent() at the reference's ER-200 test settings (train_eco.py:59-69,166-169,368-377: 50 test graphs,
-    BEST metric, every 50k env-steps).  Both measured here with HIP-synchronised wall time and amortised per
-    vector step: reset / T, evaluation x (B / test_frequency).  The reset includes regenerating B fresh graphs
-    (regenerate_graphs, the reference's new graph per episode) on slots no transition references.  Evaluations:
-    learn() runs each crossing's evaluation on ONE rank (round-robin), so the per-rank cost per vector step is
-    evaluation x (B x world / test_frequency) / world = evaluation x B / test_frequency at any world size."""
+def make_test_env(agent, dev, test_graphs=50, graph="ER", gparam=0.15):
+    """The reference's ER-200 test setting (train_eco.py:59-69, 166-169): a VecSpinSystem of 64 slots over
+    `test_graphs` seeded test graphs with the training env's arguments."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
+    return VecSpinSystem(GraphStore.random(graph, test_graphs, agent.N, gparam, seed=4321, device=dev), 64,
+                         agent.env.max_steps, **agent.env.env_args)
+
+
+def untimed_costs(agent, B, world, dev, test, test_frequency=50000):
+    """What the timed vector steps never contain (T = 2N steps per episode, 20 timed steps): the full reset of
+    all B episodes at an episode boundary (the agent's own path: fresh graph slots regenerated on the device,
+    fresh spins, compact-replay snapshot; dqn.py:306-327), and one evaluate_agent() at the reference's ER-200
+    test settings (`test`: train_eco.py:59-69,166-169,368-377: 50 test graphs, BEST metric, every 50k env-steps).
+    Both measured here with HIP-synchronised wall time and amortised per vector step.  Evaluations: learn() runs
+    ONE evaluation per test_frequency crossing for the whole job (round-robin over the ranks) and at most one
+    per vector step, so a rank runs min(1, B x world / test_frequency) / world evaluations per vector step."""
     from eco_hip.agents.dqn.utils import TestMetric
-    env, T, n = agent.env, agent.env.max_steps, agent.N
-    regen = agent.regenerate_graphs is not None and agent.graphs.n_graphs >= 2 * B
+    T = agent.env.max_steps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if regen:  # slots [B, 2B): the next batch's, not referenced by any stored transition yet
-        agent.graphs.generate(B, B, graph, gparam, seed=agent.seed + 98, check=False)
-    agent._reset_env(np.arange(B) % agent.graphs.n_graphs, agent.seed + 99)
+    agent._reset_env(agent._take_graph_slots(None), agent.seed + 99)
     torch.cuda.synchronize()
     reset_ms = (time.perf_counter() - t0) * 1e3
-    test = VecSpinSystem(GraphStore.random(graph, test_graphs, n, gparam, seed=4321, device=dev), 64, T,
-                         **env.env_args)
     saved = (agent.test_envs, agent.test_episodes, agent.test_metric)
-    agent.test_envs, agent.test_episodes, agent.test_metric = test, test_graphs, TestMetric.BEST
+    agent.test_envs, agent.test_episodes, agent.test_metric = test, test.graphs.n_graphs, TestMetric.BEST
+    agent.eval_graphs = False
     agent.evaluate_agent()  # first call: allocations
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agent.evaluate_agent()
+    torch.cuda.synchronize()
+    eval_eager_ms = (time.perf_counter() - t0) * 1e3
+    agent.eval_graphs = True
+    agent.evaluate_agent()  # eager once more, then the rollout is captured into a HIP graph
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     agent.evaluate_agent()
     torch.cuda.synchronize()
     eval_ms = (time.perf_counter() - t0) * 1e3
     # learn()'s default: the evaluation overlapped with training (DQN._evaluate_overlapped, side stream on a
-    # snapshot of the weights).  Its cost = the wall time it adds to the vector steps it runs beside.
+    # snapshot of the weights, the rollout replayed from its HIP graph).  Its cost = the wall time it adds to the
+    # vector steps it runs beside.
     k = 8
-    agent._eval_one_fill_finish(agent._evaluate_overlapped(0))  # allocations
+    for _ in range(2):  # allocations, capture
+        agent._eval_one_fill_finish(agent._evaluate_overlapped(0))
     ts = []
     for ov in (False, True, False, True):
         torch.cuda.synchronize()
@@ -384,19 +395,62 @@ def untimed_costs(agent, B, world, dev, test_graphs=50, test_frequency=50000, gr
         ts.append((time.perf_counter() - t0) * 1e3)
     ov_ms = max(0.0, (ts[1] + ts[3] - ts[0] - ts[2]) / 2)
     agent.test_envs, agent.test_episodes, agent.test_metric = saved
-    per_vec_sync = reset_ms / T + eval_ms * (B / test_frequency)
-    per_vec = reset_ms / T + ov_ms * (B / test_frequency)
-    return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T, "reset_regenerates_graphs": regen,
-            "evaluate_agent_ms": eval_ms, "evaluate_overlapped_ms": ov_ms,
+    per_vec_evals = min(1.0, B * world / test_frequency) / world
+    per_vec_sync = reset_ms / T + eval_ms * per_vec_evals
+    per_vec = reset_ms / T + ov_ms * per_vec_evals
+    return {"episode_reset_ms": reset_ms, "reset_every_vector_steps": T,
+            "reset_path": "DQN._take_graph_slots + DQN._reset_env (graph slots regenerated when free)",
+            "evaluate_agent_ms": eval_ms, "evaluate_agent_eager_launches_ms": eval_eager_ms,
+            "evaluate_overlapped_ms": ov_ms,
             "evaluate_overlapped_note": f"wall time one overlapped evaluation adds to {k} vector steps of training "
-                                        "(learn()'s default; evaluate_agent_ms is the synchronous call)",
+                                        "(learn()'s default; evaluate_agent_ms is the synchronous call replaying the "
+                                        "rollout's HIP graph, evaluate_agent_eager_launches_ms the same call with "
+                                        "~800 host launches)",
             "evaluate_every_env_steps": test_frequency,
-            "evaluate_setting": f"{test_graphs} {graph}-{n} test graphs, BEST metric, {T} greedy steps each",
+            "evaluate_setting": f"{test.graphs.n_graphs} test graphs, BEST metric, {T} greedy steps each",
+            "evaluations_per_vector_step_per_rank": per_vec_evals,
             "amortised_ms_per_vector_step": per_vec, "amortised_ms_per_vector_step_sync_eval": per_vec_sync,
-            "amortised_formula": "reset_ms / T + evaluate_overlapped_ms * (B * world / test_frequency) / world: one "
-                                 "evaluation per crossing for the whole job, dealt round-robin to the ranks "
-                                 "(DQN.learn), so the per-rank term is independent of world",
-            "note": "not in the timed region: amortised, these would add this many ms to ms_per_step"}
+            "amortised_formula": "reset_ms / T + evaluate_overlapped_ms * min(1, B * world / test_frequency) / world: "
+                                 "one evaluation per crossing for the whole job, at most one per vector step, dealt "
+                                 "round-robin to the ranks (DQN.learn)",
+            "note": "not in the timed region: amortised, these would add this many ms to ms_per_step; the learn_loop "
+                    "figure measures them end to end"}
+
+
+def learn_loop(agent, B, world, dev, test, vector_steps=60, test_frequency=50000, save_network_frequency=400000):
+    """The reference's whole training loop on the record: DQN.learn() (dqn.py:256-395) end to end, with the
+    evaluation every test_frequency env-steps on `test` (50 ER-200 graphs, BEST metric, overlapped, `_best`
+    saved; train_eco.py:368-377 cadence) and the periodic checkpoints, over `vector_steps` vector steps of all
+    ranks' B episodes.  Returns the job's env-steps/s (max wall time over ranks) and what ran."""
+    import tempfile
+    from eco_hip.agents.dqn.utils import TestMetric
+    from eco_hip.parallel import max_over_ranks
+    saved = (agent.test_envs, agent.test_episodes, agent.test_metric, agent.test_frequency, agent.evaluate,
+             agent.save_network_frequency, agent.network_save_path, agent.test_save_path)
+    timesteps = vector_steps * B * world
+    with tempfile.TemporaryDirectory() as d:
+        agent.test_envs, agent.test_episodes, agent.test_metric = test, test.graphs.n_graphs, TestMetric.BEST
+        agent.test_frequency, agent.evaluate = test_frequency, True
+        agent.save_network_frequency = save_network_frequency
+        agent.network_save_path, agent.test_save_path = os.path.join(d, "network.pth"), None
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        agent.learn(timesteps)
+        torch.cuda.synchronize()
+        dt_rank = time.perf_counter() - t0
+        n_eval = len(agent.test_scores)
+    (agent.test_envs, agent.test_episodes, agent.test_metric, agent.test_frequency, agent.evaluate,
+     agent.save_network_frequency, agent.network_save_path, agent.test_save_path) = saved
+    dt = max_over_ranks(dt_rank, device=dev)
+    return {"value": agent._timestep / dt, "unit": "env-steps/s", "env_steps": agent._timestep, "seconds": dt,
+            "vector_steps": vector_steps, "evaluations": n_eval, "test_frequency": test_frequency,
+            "save_network_frequency": save_network_frequency,
+            "what": "DQN.learn() end to end: start() (every episode reset on fresh graphs), act + env step + replay "
+                    "add + gradient steps per vector step, one evaluation per test_frequency crossing (50 test "
+                    "graphs, BEST, overlapped on a side stream, `_best` saved), periodic checkpoints, final "
+                    "collection of the scores and losses"}
 
 
 def _free_port():
@@ -639,7 +693,11 @@ def main():
     dt = max_over_ranks(dt_rank, device=dev)
     pg = process_group_info(world, dt_rank, args.steps, local, dev)
 
-    fixed = untimed_costs(agent, B, world, dev, graph=args.graph, gparam=gparam) if train else None
+    fixed = loop = None
+    if train:
+        test = make_test_env(agent, dev, graph=args.graph, gparam=gparam)
+        fixed = untimed_costs(agent, B, world, dev, test)
+        loop = learn_loop(agent, B, world, dev, test)
 
     # per-kernel roofline from the live events: forward launches vs backward launches
     kern = {"mpnn_forward_kernel": [0.0, 0.0, 0], "mpnn_backward(+wgrad)": [0.0, 0.0, 0]}
@@ -694,6 +752,9 @@ def main():
         es_rate, es_ms = envstep_rate(dev, B, n, store=store)
         out["env_step_roofline"] = envstep_roofline(es_rate, es_ms, n, B)
         out["untimed_per_episode_costs"] = fixed
+        if loop is not None:
+            loop["ratio_to_headline"] = loop["value"] / value
+            out["learn_loop"] = loop
         mf = pmc_mfma(dom, B, args.minibatch, n, args.graph, mean_gf) if train else None
         if mf:
             issued = achieved * mf["issued_per_algorithmic_flop"]

@@ -677,6 +677,15 @@ extern "C" int eco_check_errors(eco_stream_t stream) {
   return check_err_word(w, (hipStream_t)stream);
 }
 
+extern "C" int eco_error_word_copy(int32_t* dst, eco_stream_t stream) {
+  int32_t* w = err_word();
+  if (!w) return fail(ECO_ERR_HIP, "cannot allocate error word");
+  if (!dst) return fail(ECO_ERR_ARG, "null destination");
+  if (hipMemcpyAsync(dst, w, sizeof(int32_t), hipMemcpyDefault, (hipStream_t)stream) != hipSuccess)
+    return fail(ECO_ERR_HIP, "error-word copy failed");
+  return ECO_OK;
+}
+
 extern "C" int eco_env_step(const eco_env_config* cfg, const eco_graph_set* gs, void* state, int32_t batch,
                             const int32_t* actions, double* rewards, uint8_t* dones, float* obs_x, double* obs_f64,
                             eco_stream_t stream) {

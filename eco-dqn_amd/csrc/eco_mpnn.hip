@@ -1334,9 +1334,11 @@ int eco::mpnn_backward_launch(const float* packed, int32_t n_obs_in, const eco_g
 // ---- split2_pk hazard probe (the v_fma_mix inline asm carries its own wait states) ----
 namespace eco {
 // One wave per 64 x 32 block of activations: the lane's four float4 split by split2_pk (inline asm) and fed to
-// MFMAs exactly as mm_fh feeds them (order 0) or with the lo fragment consumed first, straight after the asm (order
-// 1, the schedule most exposed to a missing wait state); the same products from the plain-conversion split
-// (split2_ref).  out[2][block][4 x 16 outputs][64 lanes] fp32 accumulators, compared bitwise by the test.
+// MFMAs exactly as mm_fh feeds them (order 0), with the lo fragment consumed first, straight after the asm (order
+// 1), or with the split and that first MFMA in one asm block, the MFMA reading the register the last v_fma_mixhi
+// wrote right after the product's wait states (order 2: the only schedule where nothing else can supply them, so
+// a build without them -- ECO_SPLIT2_NEGATIVE_CONTROL -- must fail); the same products from the plain-conversion
+// split (split2_ref).  out[2][block][4 x 16 outputs][64 lanes] fp32 accumulators, compared bitwise by the test.
 template <bool REF>
 __device__ __forceinline__ void probe_split_fh(const float4& a, const float4& b, float sf, f16x8& hi, f16x8& lo) {
   uint32_t h[4], l[4];
@@ -1362,7 +1364,7 @@ __device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], 
       w1[nt] = *reinterpret_cast<const f16x8*>(wl + ((0 * 4 + nt) * 2 + kc2) * FH_FRAG);
       w2[nt] = *reinterpret_cast<const f16x8*>(wl + ((1 * 4 + nt) * 2 + kc2) * FH_FRAG);
     }
-    if (ORDER == 1) {
+    if (ORDER >= 1) {
       // order 1 places the lo fragment's first reader straight after the split's last v_fma_mixhi: all loads
       // drained and earlier MFMAs retired first (nothing for the compiler to interleave), then that first
       // MFMA as inline asm (so no compiler-inserted wait state can separate it from the asm split), followed by
@@ -1372,7 +1374,44 @@ __device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], 
     }
     __builtin_amdgcn_sched_barrier(0);
     f16x8 xh, xl;
-    probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+    if (ORDER == 2 && !REF) {
+      // order 2: the split's eight v_fma_mix (the product's asm text and wait states, ECO_MIXLO / ECO_MIXHI /
+      // ECO_SPLIT2_WAIT) and the first MFMA reading its lo fragment in ONE asm block with fixed registers, the MFMA
+      // straight after the v_fma_mixhi that wrote its last operand register: nothing the compiler schedules can
+      // separate them, so only ECO_SPLIT2_WAIT stands between the write and the read.  The lo pieces are then
+      // copied out for the remaining MFMAs.
+      const float v[8] = {x[2 * kc2].x, x[2 * kc2].y, x[2 * kc2].z, x[2 * kc2].w,
+                          x[2 * kc2 + 1].x, x[2 * kc2 + 1].y, x[2 * kc2 + 1].z, x[2 * kc2 + 1].w};
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) h[t] = pk_f16(v[2 * t] * sf, v[2 * t + 1] * sf);
+      asm volatile("s_nop 4\n\t"  // the compiler's VALU writes of h / v before this asm (reads by VALU: none needed)
+                   ECO_MIXLO("v200", "%[a0]", "%[sf]", "%[h0]") "\n\t" ECO_MIXLO("v201", "%[a2]", "%[sf]", "%[h1]") "\n\t"
+                   ECO_MIXLO("v202", "%[a4]", "%[sf]", "%[h2]") "\n\t" ECO_MIXLO("v203", "%[a6]", "%[sf]", "%[h3]") "\n\t"
+                   ECO_MIXHI("v200", "%[a1]", "%[sf]", "%[h0]") "\n\t" ECO_MIXHI("v201", "%[a3]", "%[sf]", "%[h1]") "\n\t"
+                   ECO_MIXHI("v202", "%[a5]", "%[sf]", "%[h2]") "\n\t" ECO_MIXHI("v203", "%[a7]", "%[sf]", "%[h3]")
+                   ECO_SPLIT2_WAIT "\n\t"
+                   "v_mfma_f32_16x16x32_f16 %[acc], %[w], v[200:203], %[acc]\n\t"
+                   "v_mov_b32 %[l0], v200\n\tv_mov_b32 %[l1], v201\n\tv_mov_b32 %[l2], v202\n\tv_mov_b32 %[l3], v203\n\t"
+                   "s_nop 7\n\ts_nop 7\n\ts_nop 3"
+                   : [acc] "+v"(acc[0]), [l0] "=&v"(l[0]), [l1] "=&v"(l[1]), [l2] "=&v"(l[2]), [l3] "=&v"(l[3])
+                   : [w] "v"(w1[0]), [sf] "v"(sf), [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]),
+                     [a0] "v"(v[0]), [a1] "v"(v[1]), [a2] "v"(v[2]), [a3] "v"(v[3]), [a4] "v"(v[4]), [a5] "v"(v[5]),
+                     [a6] "v"(v[6]), [a7] "v"(v[7])
+                   : "v200", "v201", "v202", "v203");
+      const u32x4v hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+      xh = __builtin_bit_cast(f16x8, hv);
+      xl = __builtin_bit_cast(f16x8, lv);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      probe_split_fh<REF>(x[2 * kc2], x[2 * kc2 + 1], sf, xh, xl);
+    }
+    if (ORDER == 2 && REF) {  // the same first product from the plain split (compiler VALU: wait states written out)
+      asm volatile("s_nop 4\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                   : "+v"(acc[0])
+                   : "v"(w1[0]), "v"(xl));
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (ORDER == 1) {
       // (the plain-conversion reference split is compiler VALU code: its wait states before this asm MFMA are
       // written out here, the recognizer not knowing the asm is an MFMA; the asm split carries its own)
@@ -1388,7 +1427,7 @@ __device__ __forceinline__ void probe_mm(f32x4 (&acc)[4], const float4 (&x)[4], 
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      if (ORDER == 1 && nt == 0) {
+      if (ORDER >= 1 && nt == 0) {
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w2[0], xh, acc[0], 0, 0, 0);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[0], xh, acc[0], 0, 0, 0);
       } else if (ORDER == 0) {  // mm_fh
@@ -1436,11 +1475,12 @@ __global__ __launch_bounds__(256) void split2_probe_kernel(const float* x, const
 extern "C" int eco_probe_split2_mfma(const float* x, const float* sf, const uint16_t* w_frags, int32_t n_blocks,
                                      int32_t order, float* out, eco_stream_t stream) {
   using namespace eco;
-  if (!x || !sf || !w_frags || !out || n_blocks < 1 || (order != 0 && order != 1))
+  if (!x || !sf || !w_frags || !out || n_blocks < 1 || order < 0 || order > 2)
     return fail(ECO_ERR_ARG, "eco_probe_split2_mfma: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const int grid = (n_blocks + 3) / 4;
   if (order == 0) split2_probe_kernel<0><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
-  else split2_probe_kernel<1><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
+  else if (order == 1) split2_probe_kernel<1><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
+  else split2_probe_kernel<2><<<grid, 256, 0, st>>>(x, sf, w_frags, out, n_blocks);
   return check_launch("split2_probe");
 }

@@ -68,17 +68,22 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
 // lo = fp16(a sf - hi) in ONE v_fma_mix{lo,hi}_f16 per value (f32 a and sf, f16 hi, single rounding: a sf - hi
 // is exact, so the result is bitwise that of converting hi back, subtracting and converting: 4 VALU per pair
 // instead of 6, the per-layer split being the largest VALU item of the dense kernels)
+// The asm text, shared with the hazard probe (eco_probe_split2_mfma order 2, which places an MFMA reading the
+// register straight after the last v_fma_mixhi): d = a sf - h, written to the low / high half of d.
+#define ECO_MIXLO(d, a, s, h) "v_fma_mixlo_f16 " d ", " a ", " s ", -" h " op_sel_hi:[0,0,1]"
+#define ECO_MIXHI(d, a, s, h) "v_fma_mixhi_f16 " d ", " a ", " s ", -" h " op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+// the trailing wait states: the hazard recognizer does not see inside inline asm, and an MFMA reading a VGPR
+// written by VALU needs 2 (without them the fragments fed to the MFMAs were stale in some schedules)
+#ifndef ECO_SPLIT2_NEGATIVE_CONTROL
+#define ECO_SPLIT2_WAIT "\n\ts_nop 1"
+#else  // tests/test_split2_hazard_gpu.py's negative control (a tools build only): the wait states removed
+#define ECO_SPLIT2_WAIT ""
+#endif
 __device__ __forceinline__ void split2_pk(float a, float b, float sf, uint32_t& hi, uint32_t& lo) {
   hi = pk_f16(a * sf, b * sf);
   uint32_t l;  // mixlo writes bits 15:0 (16:31 kept, then written by mixhi)
-  // the trailing s_nop: the hazard recognizer does not see inside inline asm, and an MFMA reading a VGPR written
-  // by VALU needs 2 wait states (without it the fragments fed to the MFMAs were stale in some schedules)
-  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(sf), "v"(hi));
-#ifndef ECO_SPLIT2_NEGATIVE_CONTROL
-  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1" : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
-#else  // tests/test_split2_hazard_gpu.py's negative control (a tools build only): the wait states removed
-  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
-#endif
+  asm(ECO_MIXLO("%0", "%1", "%2", "%3") : "=v"(l) : "v"(a), "v"(sf), "v"(hi));
+  asm(ECO_MIXHI("%0", "%1", "%2", "%3") ECO_SPLIT2_WAIT : "+v"(l) : "v"(b), "v"(sf), "v"(hi));
   lo = l;
 }
 // the same split by plain conversions (v_cvt_pk_f16_f32, f32 subtract, convert): the reference of

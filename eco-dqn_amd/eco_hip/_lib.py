@@ -81,6 +81,7 @@ _SIG = {
                                     _P, _P]),
     "eco_env_read": (ctypes.c_int, [ctypes.POINTER(EnvConfig), _P, _I, _P, _P, _P, _P]),
     "eco_check_errors": (ctypes.c_int, [_P]),
+    "eco_error_word_copy": (ctypes.c_int, [_P, _P]),
     "eco_set_kernel_paths": (_I, [_I]),
     "eco_probe_split2_mfma": (ctypes.c_int, [_P, _P, _P, _I, _I, _P, _P]),
     "eco_env_greedy_actions": (ctypes.c_int, [ctypes.POINTER(EnvConfig), ctypes.POINTER(GraphSet), _P, _I, _P,

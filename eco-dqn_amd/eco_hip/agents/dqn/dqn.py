@@ -188,6 +188,10 @@ class DQN:
         # training continues (same results: the snapshot is the network at the evaluation's timestep)
         self.overlap_evaluation = overlap_evaluation
         self._eval_stream = None
+        # one-fill evaluations replay their rollout from a HIP graph captured at the second evaluation of an
+        # (env, network) pair (_capture_eval_rollout); False keeps every evaluation's launches eager
+        self.eval_graphs = True
+        self._eval_graphs = {}
 
         self._act_counter = 0
         self._alloc_train_buffers(self.M)
@@ -321,8 +325,8 @@ class DQN:
         kind, param = self.regenerate_graphs[:2]
         weights = self.regenerate_graphs[2] if len(self.regenerate_graphs) > 2 else "discrete"
         n_slots = len(self._slot_users)
-        if self._started:   # release the slots of the episodes being reset
-            old = self.env.graph_ids.cpu().numpy()
+        if self._started:   # release the slots of the episodes being reset (host mirror: no device read)
+            old = self._host_graph_ids
             old = old if episodes is None else old[episodes]
             np.subtract.at(self._slot_users, old, 1)
             self._slot_free_at[old[self._slot_users[old] == 0]] = self._pushed
@@ -364,7 +368,14 @@ class DQN:
         return nxt
 
     def _reset_env(self, graph_ids, seed, mask=None):
-        """env.reset (all episodes, or the masked ones) and, for the compact replay, record the new states."""
+        """env.reset (all episodes, or the masked ones) and, for the compact replay, record the new states.
+        The episodes' graph ids are mirrored on the host for the slot bookkeeping of _take_graph_slots."""
+        ids = np.asarray(graph_ids, np.int64)
+        if mask is None or not hasattr(self, "_host_graph_ids"):
+            self._host_graph_ids = ids.copy()
+        else:
+            m = np.asarray(mask.cpu() if torch.is_tensor(mask) else mask).astype(bool)
+            self._host_graph_ids[m] = ids[m]
         self.env.reset(graph_ids=graph_ids, mask=mask, seed=seed)
         if self.compact_replay:
             self.replay_buffer.snapshot(mask)
@@ -458,63 +469,133 @@ class DQN:
 
         Multi-GPU: each crossing is ONE evaluation of the job, run by one rank (evaluation e by rank e mod world,
         on its test env: the same episodes and test graphs as a single-process evaluation at that timestep); its
-        scores reach every rank through a small all-reduce at a fixed point (when evaluation e + world starts, or
-        at the end of learn()), so the evaluation work per rank per vector step does not grow with the world
-        size.  Rank 0 keeps a copy of the weights of every evaluation in flight for `_best` (the parameters are
-        bit-identical across ranks).
+        scores reach every rank through a small all-reduce to which only the owner contributes, issued by every
+        rank at the same point (when evaluation e + world starts, or at the end of learn()), so the evaluation
+        work per rank per vector step does not grow with the world size.  Nothing here waits for the training
+        stream: the all-reduce is asynchronous and its result is read back into pinned memory behind an event,
+        recorded (scores, `_best`) once that event has fired -- a few vector steps later -- or at the end; the
+        owner's scores come from pinned copies behind the side stream's event; the regenerated graphs' error word
+        is peeked the same way (eco_error_word_copy).  Rank 0 snapshots the weights of every evaluation into
+        pinned host memory at its timestep for `_best` (the parameters are bit-identical across ranks).
         Returns the last 100 (timestep, loss) pairs."""
         import pickle
         from collections import deque
         self.start()
         rank = torch.distributed.get_rank() if self.dist else 0
         world = self.world
+        nccl = world > 1 and torch.distributed.get_backend() == "nccl"
         test_scores, test_solutions = [], []
-        inflight = deque()   # evaluations launched, not yet recorded (index order)
+        inflight = deque()   # evaluations launched, scores not yet taken (index order)
+        reducing = deque()   # scores taken, all-reduce / read-back in flight, not yet recorded (index order)
+        err_checks = deque()  # (event, pinned word) peeks at the device error word
+        saves = deque()      # (event, pinned weights, path) periodic checkpoints not yet written
         n_eval = 0           # evaluations launched by the job so far (every rank counts the same)
         test_env0 = self._test_env() if self.evaluate else None
         cursor0 = getattr(test_env0, "_eval_next_graph", 0) if test_env0 is not None else 0
+        # rank 0's weight snapshots for _best, one pinned slot per evaluation that can be unrecorded at once
+        depth = 3 * world
+        snaps = ([torch.empty(self.network.flat.numel(), dtype=torch.float32).pin_memory() for _ in range(depth)]
+                 if rank == 0 and self.evaluate else None)
 
-        def record(tk, test_score, test_solution, net):
+        def record(e, test_score, test_solution):
             if verbose and rank == 0:
                 print('\nTest score: {}\nTest solution: {}\n'.format(np.round(test_score, 3),
                                                                     np.round(test_solution, 3)))
             if all(test_score > sc for _, sc in test_scores) and rank == 0:
                 main, ext = os.path.splitext(self.network_save_path)
-                self.save(main + "_best" + (ext or ".pth"), network=net)
-            test_scores.append([tk, test_score])
-            test_solutions.append([tk, test_solution])
+                e["snap_ev"].synchronize()  # the snapshot copy (issued at the evaluation's timestep) has landed
+                self._save_flat(main + "_best" + (ext or ".pth"), e["snap"])
+            test_scores.append([e["tk"], test_score])
+            test_solutions.append([e["tk"], test_solution])
 
-        def collect(e):
-            """Record evaluation e on every rank (the same call order everywhere: the all-reduce is collective)."""
+        def take(e):
+            """Evaluation e's scores on every rank (the same call order everywhere: the all-reduce is collective):
+            the owner's from its pinned results, all-reduced without waiting; recorded by flush()."""
             if e["owner"] == rank:
                 sc, so = self._eval_one_fill_finish(e["p"]) if "p" in e else e["result"]
             else:
                 sc, so = 0.0, 0.0
-            if world > 1:
-                t = torch.tensor([sc, so], dtype=torch.float64,
-                                 device=self.device if torch.distributed.get_backend() == "nccl" else "cpu")
-                torch.distributed.all_reduce(t)  # only the owner contributes: the sum is its result
-                sc, so = float(t[0]), float(t[1])
-            record(e["tk"], sc, so, e["net"])
+            if world == 1:
+                record(e, sc, so)
+                return
+            src = torch.tensor([sc, so], dtype=torch.float64).pin_memory()
+            if nccl:
+                t = torch.empty(2, dtype=torch.float64, device=self.device)
+                t.copy_(src, non_blocking=True)
+            else:
+                t = src
+            work = torch.distributed.all_reduce(t, async_op=True)  # only the owner contributes: the sum is its result
+            e["red"] = (src, t, work)
+            if nccl:
+                work.wait()  # the current stream waits for the collective; the host does not
+                e["res"] = torch.empty(2, dtype=torch.float64).pin_memory()
+                e["res"].copy_(t, non_blocking=True)
+                e["res_ev"] = torch.cuda.Event()
+                e["res_ev"].record()
+            reducing.append(e)
+
+        def flush(upto):
+            """Record, in order, the reduced evaluations whose results have arrived, waiting for those with
+            index <= upto (None: wait for none)."""
+            while reducing:
+                e = reducing[0]
+                src, t, work = e["red"]
+                must = upto is not None and e["idx"] <= upto
+                if nccl:
+                    if not (must or e["res_ev"].query()):
+                        return
+                    e["res_ev"].synchronize()
+                    res = e["res"]
+                else:
+                    if not (must or work.is_completed()):
+                        return
+                    work.wait()
+                    res = t
+                reducing.popleft()
+                record(e, float(res[0]), float(res[1]))
+
+        def save_deferred(path, block):
+            """Periodic checkpoints: the weights copied into pinned memory at their timestep, written once the
+            copy has landed (no wait on the training stream)."""
+            if path is not None:
+                host = torch.empty(self.network.flat.numel(), dtype=torch.float32).pin_memory()
+                host.copy_(self.network.flat, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                saves.append((ev, host, path))
+            while saves and (block or saves[0][0].query()):
+                ev, host, p_ = saves.popleft()
+                ev.synchronize()
+                self._save_flat(p_, host)
+
+        def peek_errors(block):
+            """Raise a device error flagged since the last peek (regenerated graphs: edge-slot overflow)."""
+            while err_checks and (block or err_checks[0][0].query()):
+                ev, word = err_checks.popleft()
+                ev.synchronize()
+                if int(word[0]) != 0:
+                    self.graphs.check_errors()
 
         def launch(tk):
             nonlocal n_eval
             owner = n_eval % world
-            e = {"tk": tk, "owner": owner, "idx": n_eval, "net": None}
+            e = {"tk": tk, "owner": owner, "idx": n_eval}
             n_eval += 1
+            if rank == 0:
+                # slot idx % depth is free once evaluation idx - depth is recorded (launched >= 2 world earlier)
+                flush(e["idx"] - depth)
+                e["snap"] = snaps[e["idx"] % depth]
+                e["snap"].copy_(self.network.flat, non_blocking=True)  # the weights at tk, for _best
+                e["snap_ev"] = torch.cuda.Event()
+                e["snap_ev"].record()
             if owner == rank:
                 env = self._test_env()
                 n_graphs = env.graphs.n_graphs
                 env._eval_next_graph = (cursor0 + e["idx"] * self.test_episodes) % n_graphs  # job-wide order
                 if self._overlap_ok(env):
                     e["p"] = self._evaluate_overlapped(tk)
-                    e["net"] = e["p"]["net"]
                 else:
                     e["result"] = self.evaluate_agent()
-            if rank == 0 and e["net"] is None:  # the weights at tk, for _best (recorded after more training)
-                snap = self._network_factory()
-                snap.flat.copy_(self.network.flat)
-                e["net"] = snap
             inflight.append(e)
 
         while self._timestep < timesteps:
@@ -527,22 +608,32 @@ class DQN:
                 continue
             crossed_test = t // self.test_frequency > t_prev // self.test_frequency
             if crossed_test and self.regenerate_graphs is not None:
-                # graphs regenerated with check=False since the last sync point: an edge-slot overflow
-                # sets the device error word (the slot becomes an empty graph); surface it here
-                self.graphs.check_errors()
+                # graphs regenerated with check=False since the last peek: an edge-slot overflow sets the device
+                # error word (the slot becomes an empty graph); peeked without waiting, raised when seen
+                word = torch.zeros(1, dtype=torch.int32).pin_memory()
+                _lib.check(_lib.lib.eco_error_word_copy(_lib.ptr(word), _lib.stream_ptr()))
+                ev = torch.cuda.Event()
+                ev.record()
+                err_checks.append((ev, word))
+            peek_errors(False)
+            flush(None)
+            save_deferred(None, False)
             if world == 1 and inflight and "p" in inflight[0] and inflight[0]["p"]["done"].query():
-                collect(inflight.popleft())  # finished early (one process: no collective to keep in step)
+                take(inflight.popleft())  # finished early (one process: no collective to keep in step)
             if self.evaluate and crossed_test:
                 tk = (t // self.test_frequency) * self.test_frequency
                 while len(inflight) >= world:  # this evaluation's owner runs one evaluation at a time
-                    collect(inflight.popleft())
+                    take(inflight.popleft())
                 launch(tk)
             if t // self.save_network_frequency > t_prev // self.save_network_frequency and rank == 0:
                 tk = (t // self.save_network_frequency) * self.save_network_frequency
                 main, ext = os.path.splitext(self.network_save_path)
-                self.save(main + str(tk) + (ext or ".pth"))
+                save_deferred(main + str(tk) + (ext or ".pth"), False)
         while inflight:
-            collect(inflight.popleft())
+            take(inflight.popleft())
+        flush(n_eval)
+        peek_errors(True)
+        save_deferred(None, True)
         if self.regenerate_graphs is not None:
             self.graphs.check_errors()
         losses = self.losses()
@@ -686,42 +777,101 @@ class DQN:
         refill loop, issued with no host synchronisation (on the current stream).  The k episodes take slots
         0..k-1, so each prediction's batch (its norm.max() coupling, dqn.py:546-547) is the contiguous prefix
         obs_x[:k] -- all of them are active until the last step, as in the refill loop."""
-        dev = self.device
         k = self.test_episodes
         n_graphs = env.graphs.n_graphs
         if not hasattr(env, "_eval_next_graph"):
             env._eval_next_graph = 0
-        # every slot holds a valid episode (unused ones run to their end and stay masked), as evaluate_agent
-        env.reset(graph_ids=np.arange(env.n_envs) % n_graphs, seed=self.eval_seed)
-        mask = np.zeros(env.n_envs, dtype=np.uint8)
-        mask[:k] = 1
-        gids = np.zeros(env.n_envs, dtype=np.int64)
-        gids[:k] = (env._eval_next_graph + np.arange(k)) % n_graphs
-        env._eval_next_graph = (env._eval_next_graph + k) % n_graphs
-        env.reset(graph_ids=gids, mask=mask, seed=self.eval_seed)
-        cum = torch.zeros(env.n_envs, dtype=torch.float64, device=dev)
         keep_cum = self.test_metric == TestMetric.CUMULATIVE_REWARD
-        acts = torch.zeros(env.n_envs, dtype=torch.int32, device=dev)
-        sub = acts[:k]
         act_cfg.counter = 0
+        net._ensure_packed()
+        rec = self._eval_rollout_record(env, act_cfg, net, k, keep_cum)
+        # the resets' graph ids and mask are formed on the device (no host upload, no synchronisation): every slot
+        # holds a valid episode (unused ones run to their end and stay masked), as evaluate_agent, then slots
+        # 0..k-1 take the next k test graphs
+        slot = rec["slot"]
+        env.reset(graph_ids=slot % n_graphs, seed=self.eval_seed)
+        env.reset(graph_ids=(slot + env._eval_next_graph) % n_graphs, mask=rec["mask"], seed=self.eval_seed)
+        env._eval_next_graph = (env._eval_next_graph + k) % n_graphs
+        if keep_cum:
+            rec["cum"].zero_()
+        if rec["graph"] is not None:
+            rec["graph"].replay()
+        else:
+            self._eval_rollout(env, act_cfg, net, k, rec)
+            rec["eager_runs"] += 1
+            if self.eval_graphs and net.timer is None:
+                self._capture_eval_rollout(env, act_cfg, net, k, rec)
+        env.read()
+        # the results into pinned host memory behind the rollout (read by _eval_one_fill_finish once the stream's
+        # event has fired: no device read on the training stream)
+        rec["host_scalars"].copy_(env.scalars, non_blocking=True)
+        if keep_cum:
+            rec["host_cum"].copy_(rec["cum"], non_blocking=True)
+        return {"env": env, "k": k, "cum": rec["host_cum"], "st": env.scalar_fields(rec["host_scalars"]),
+                "metric": self.test_metric}
+
+    def _eval_rollout(self, env, act_cfg, net, k, rec):
+        """The one-fill evaluation's max_steps greedy steps: forward + fused greedy act over the k episodes, then
+        the env step of every slot (dqn.py:536-558 without the host round trips)."""
+        acts, cum = rec["acts"], rec["cum"]
+        sub = acts[:k]
         scope = _lib.ECO_NORM_PER_CALL  # the batch obs_x[:k] never changes: its max degree once, then reused
         for _ in range(env.max_steps):
             net.forward_graphs(env.obs_x[:k], env.graphs, env.graph_ids[:k], norm_scope=scope,
                                act=act_cfg, actions_out=sub)
             _, rew, _ = env.step(acts)
             scope = _lib.ECO_NORM_PER_CALL_REUSE
-            if keep_cum:  # only the cumulative-reward metric reads it: one elementwise launch fewer per step
+            if rec["keep_cum"]:  # only the cumulative-reward metric reads it: one elementwise launch fewer per step
                 cum += rew
-        st = env.read()  # device scalars; read by _eval_one_fill_finish
-        return {"env": env, "k": k, "cum": cum, "st": st, "metric": self.test_metric}
+
+    @staticmethod
+    def _eval_rollout_key(env, act_cfg, net, k, keep_cum):
+        """Everything the captured rollout's kernel arguments depend on: the buffers' device addresses (a
+        reallocated workspace or feature buffer needs a new capture) and the act / env configuration."""
+        ws = net._workspace(env.n_spins, k)
+        ptrs = tuple(int(t.data_ptr()) if t is not None else 0 for t in
+                     (env.obs_x, env.obs_f64, env.state, env.rewards, env.dones, env.graph_ids, net.packed, ws))
+        return (ptrs, bytes(env.graphs.gs), bytes(env.cfg), env.n_envs, k, keep_cum, float(act_cfg.epsilon),
+                int(act_cfg.reversible), float(act_cfg.allowed_value), int(act_cfg.seed))
+
+    def _eval_rollout_record(self, env, act_cfg, net, k, keep_cum):
+        """The (env, network) pair's rollout record: persistent action / cumulative-reward buffers and, from the
+        second evaluation on, the HIP graph of the rollout's 2 x max_steps launches.  The record holds the env and
+        the network (so every address the graph names stays allocated); a changed key drops the old graph."""
+        key = self._eval_rollout_key(env, act_cfg, net, k, keep_cum)
+        pair = (id(env), id(net))
+        rec = self._eval_graphs.get(pair)
+        if rec is None or rec["key"] != key:
+            dev = self.device
+            slot = torch.arange(env.n_envs, dtype=torch.int32, device=dev)
+            rec = {"key": key, "env": env, "net": net, "graph": None, "eager_runs": 0, "keep_cum": keep_cum,
+                   "acts": torch.zeros(env.n_envs, dtype=torch.int32, device=dev),
+                   "cum": torch.zeros(env.n_envs, dtype=torch.float64, device=dev),
+                   "slot": slot, "mask": (slot < k).to(torch.uint8),
+                   "host_scalars": torch.zeros(env.scalars.shape, dtype=torch.float64).pin_memory(),
+                   "host_cum": torch.zeros(env.n_envs, dtype=torch.float64).pin_memory()}
+            self._eval_graphs[pair] = rec
+        return rec
+
+    def _capture_eval_rollout(self, env, act_cfg, net, k, rec):
+        """Capture the rollout (2 x max_steps launches) into a HIP graph, replayed by the next evaluations of this
+        (env, network) pair: one graph launch instead of ~800 host launches of ~20-30 us each, which otherwise
+        leave the training stream without queued work while an overlapped evaluation is issued.  Captured after an
+        eager run (workspaces allocated, kernels loaded); the capture itself executes nothing."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._eval_rollout(env, act_cfg, net, k, rec)
+        rec["graph"] = g
 
     def _eval_one_fill_finish(self, p):
         """Scores of a launched one-fill evaluation, listed in completion order (end step, then slot), as the
         refill loop appends them."""
         env, k, cum, st, metric = p["env"], p["k"], p["cum"], p["st"], p["metric"]
-        if p.get("done") is not None:
-            p["done"].synchronize()
-        ends = st["current_step"][:k].cpu().numpy()
+        if p.get("done") is None:  # a synchronous evaluation: its copies were issued on the current stream
+            p["done"] = torch.cuda.Event()
+            p["done"].record()
+        p["done"].synchronize()  # the host copies have landed (the side stream's work only)
+        ends = st["current_step"][:k].numpy()
         order = np.lexsort((np.arange(k), ends))
         scores, solutions = [], []
         for i in order.tolist():
@@ -785,6 +935,18 @@ class DQN:
         return 0.0 if invalid else size
 
     # ------------------------------------------------------------ checkpoint
+    def _save_flat(self, path, flat):
+        """save() of a parameter vector in state_dict order (a host copy of MPNN.flat): the same keys and
+        tensors as the network's state_dict (mpnn.MPNN.flat views)."""
+        from ...networks.mpnn import param_layout
+        sd, off = {}, 0
+        for name, shape in param_layout(self.network.n_obs_in):
+            cnt = int(np.prod(shape))
+            sd[name] = flat[off:off + cnt].view(shape).clone()
+            off += cnt
+        assert off == flat.numel()
+        torch.save(sd, path)
+
     def save(self, path='network.pth', network=None):
         """dqn.py:604-607: torch.save(state_dict) -- loadable by the reference MPNN.  The reference's
         extension fix-up is a no-op expression (`path + '.pth'`, :606), so `path` is used as given.

@@ -8,6 +8,7 @@ observations, see tests/test_env_gpu.py).
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from .. import _lib
@@ -97,20 +98,29 @@ class VecSpinSystem:
     def _s(self):
         return _lib.stream_ptr(self.stream)
 
+    def _upload(self, a, dtype):
+        """Host or device array -> contiguous device tensor of `dtype`, without a host synchronisation: host data
+        goes through pinned memory (torch's caching host allocator keeps the block until the copy has run) and
+        a non-blocking copy on the current stream."""
+        dev = self.graphs.device
+        if isinstance(a, torch.Tensor) and a.is_cuda:
+            return a.to(device=dev, dtype=dtype).contiguous()
+        t = torch.as_tensor(np.asarray(a.cpu() if isinstance(a, torch.Tensor) else a)).to(dtype).contiguous()
+        return t.pin_memory().to(dev, non_blocking=True)
+
     def reset(self, graph_ids=None, spins=None, mask=None, seed=0, obs_out=None):
-        if graph_ids is not None:
-            gi = torch.as_tensor(graph_ids, dtype=torch.int32, device=self.graphs.device)
-            if mask is None:
-                self.graph_ids.copy_(gi)
-            else:
-                m = torch.as_tensor(mask, device=self.graphs.device).bool()
-                self.graph_ids[m] = gi[m]
-        sp = None
-        if spins is not None:
-            sp = torch.as_tensor(spins, dtype=torch.int8, device=self.graphs.device).contiguous()
         mk = None
         if mask is not None:
-            mk = torch.as_tensor(mask, dtype=torch.uint8, device=self.graphs.device).contiguous()
+            mk = self._upload(mask, torch.uint8)
+        if graph_ids is not None:
+            gi = self._upload(graph_ids, torch.int32)
+            if mask is None:
+                self.graph_ids.copy_(gi)
+            else:  # graph_ids[mask] = gi[mask] without the host round trip of boolean indexing
+                self.graph_ids.copy_(torch.where(mk.bool(), gi, self.graph_ids))
+        sp = None
+        if spins is not None:
+            sp = self._upload(spins, torch.int8)
         if obs_out is not None:
             self.obs_x = obs_out
         _lib.check(_lib.lib.eco_env_reset(ctypes.byref(self.cfg), ctypes.byref(self.graphs.gs),
@@ -120,7 +130,7 @@ class VecSpinSystem:
         if mask is None:
             self.dones.zero_()
         else:
-            self.dones[mk.bool()] = 0
+            self.dones.masked_fill_(mk.bool(), 0)
         return self.obs_x
 
     def step(self, actions, obs_out=None):
@@ -155,16 +165,20 @@ class VecSpinSystem:
         bs = torch.zeros(self.n_envs, self.n_spins, dtype=torch.int8, device=dev) if best_spins else None
         _lib.check(_lib.lib.eco_env_read(ctypes.byref(self.cfg), _lib.ptr(self.state), self.n_envs,
                                          _lib.ptr(self.scalars), _lib.ptr(sp), _lib.ptr(bs), self._s()))
-        s = self.scalars
-        out = dict(current_step=s[:, 0], score=s[:, 1], normalized_score=s[:, 2], best_score=s[:, 3],
-                   best_score_normalized=s[:, 4], best_solution=s[:, 5], hamming=s[:, 6], done=s[:, 7],
-                   max_local_reward=s[:, 8], quality_normalizer=s[:, 9], invalidity_normalizer=s[:, 10],
-                   lower_bound=s[:, 11], set_size=s[:, 12], invalidity=s[:, 13])
+        out = self.scalar_fields(self.scalars)
         if spins:
             out["spins"] = sp
         if best_spins:
             out["best_spins"] = bs
         return out
+
+    @staticmethod
+    def scalar_fields(s):
+        """The named columns of an [n_envs, ECO_ENV_SCALARS] float64 scalar block (eco_env_read), device or host."""
+        return dict(current_step=s[:, 0], score=s[:, 1], normalized_score=s[:, 2], best_score=s[:, 3],
+                    best_score_normalized=s[:, 4], best_solution=s[:, 5], hamming=s[:, 6], done=s[:, 7],
+                    max_local_reward=s[:, 8], quality_normalizer=s[:, 9], invalidity_normalizer=s[:, 10],
+                    lower_bound=s[:, 11], set_size=s[:, 12], invalidity=s[:, 13])
 
     def allowed_action_value(self):
         """get_allowed_action_states (spinsystem.py:576-593) for irreversible envs: the

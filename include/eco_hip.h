@@ -258,7 +258,9 @@ int32_t eco_set_kernel_paths(int32_t mask);
  * v_fma_mix split, which carries its own MFMA wait states -- src/networks/mpnn.py:111-118 is the Linear it feeds).
  * n_blocks blocks of 64 nodes x 16 fp32 activations x[n_blocks][64][16], per-block power-of-two scale sf[n_blocks],
  * one 64-input half of fp16x2 weight fragments w_frags (16 fragments of 512 fp16, the PK_FH layout); order 0 feeds
- * the MFMAs as the dense kernels do, order 1 consumes the lo piece first.  out[2][n_blocks][16][64]: the fp32
+ * the MFMAs as the dense kernels do, order 1 consumes the lo piece first, order 2 issues the split and the first
+ * MFMA reading its lo piece in one asm block (the MFMA straight after the split's own wait states, nothing between
+ * them that the compiler could schedule).  out[2][n_blocks][16][64]: the fp32
  * accumulators from the asm split, then from a plain-conversion split -- bitwise equal when the split is sound. */
 int eco_probe_split2_mfma(const float *x, const float *sf, const uint16_t *w_frags, int32_t n_blocks, int32_t order,
                           float *out, eco_stream_t stream);
@@ -384,6 +386,11 @@ int eco_replay_gather(const eco_replay *rb, int32_t m, const int32_t *slots, flo
  * recorded in a device word by the asynchronous kernels; this synchronises
  * `stream`, returns and clears the first one (ECO_OK if none). */
 int eco_check_errors(eco_stream_t stream);
+/* Asynchronous peek at the same device word: enqueue a copy of it into *dst (pinned host or device memory) on
+ * `stream`, without synchronising or clearing it.  A caller that must not block (DQN.learn's per-evaluation check of
+ * the regenerated graphs, dqn.py:349-364 cadence) reads *dst once an event behind the copy has fired and calls
+ * eco_check_errors only when it is nonzero. */
+int eco_error_word_copy(int32_t *dst, eco_stream_t stream);
 
 /* Thread-local text of the last error. */
 const char *eco_last_error(void);

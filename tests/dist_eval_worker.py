@@ -2,7 +2,8 @@
 DQN.learn() with evaluations over gloo, both ranks on GPU 0.  B x world = 256 env-steps per vector step against
 test_frequency = 200, so EVERY vector step crosses a test point (the regime of configs[3] at 8 GPUs).  Each
 crossing must be one evaluation of the job (owner = evaluation index mod world), every rank must record the same
-test scores, and the `_best` checkpoint rank 0 writes must reproduce the best recorded score when evaluated again.
+test scores, and the `_best` checkpoint rank 0 writes must reproduce the best recorded score when evaluated again on the graphs of
+that evaluation's job-wide index.  learn()'s steady state must not synchronise the host with the device.
 Rank 0 prints EVAL_OK <evaluations> <per-rank counts> <best score>."""
 import os
 import sys
@@ -34,8 +35,9 @@ def main():
               basin_reward=1. / n)
     store = GraphStore.random("ER", 512, n, 0.15, seed=60 + rank, device="cuda:0")
     env = VecSpinSystem(store, B, 2 * n, **kw)
-    # the same test graphs on every rank (train_eco.py's fixed test set)
-    test = VecSpinSystem(GraphStore.random("ER", 10, n, 0.15, seed=777, device="cuda:0"), 16, 2 * n, **kw)
+    # the same test graphs on every rank (train_eco.py's fixed test set); more graphs (25) than episodes per
+    # evaluation (10), so each evaluation's graphs depend on its job-wide index (cursor0 + idx x 10 mod 25)
+    test = VecSpinSystem(GraphStore.random("ER", 25, n, 0.15, seed=777, device="cuda:0"), 16, 2 * n, **kw)
     tmp = tempfile.mkdtemp(prefix=f"eco_eval_r{rank}_")
     agent = DQN(env, lambda: MPNN(device="cuda:0"), init_weight_std=0.01, double_dqn=True, replay_start_size=2 * B,
                 replay_buffer_size=4096, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
@@ -45,7 +47,29 @@ def main():
                 test_metric=TestMetric.BEST, test_save_path=os.path.join(tmp, "scores"),
                 network_save_path=os.path.join(tmp, "net.pth"), save_network_frequency=10 ** 9)
     timesteps = B * world * 2 * n * 2
-    agent.learn(timesteps=timesteps)
+    # no host synchronisation inside learn()'s steady state: torch's sync-debug mode raises on any implicit
+    # device synchronisation (item(), cpu(), blocking copies, stream / device synchronize) from the 4th vector
+    # step after training is ready (the first evaluation of each rank has captured its rollout graph by then)
+    # to the last one, and the device error check (eco_check_errors) must not be called meanwhile
+    steady = {"n": 0, "on": False, "checks": 0}
+    real_check = agent.graphs.check_errors
+
+    def counting_check(*a, **k):
+        if steady["on"]:
+            steady["checks"] += 1
+        return real_check(*a, **k)
+    agent.graphs.check_errors = counting_check
+
+    def on_step(t):
+        if agent._ready:
+            steady["n"] += 1
+        on = 4 <= steady["n"] and t < timesteps
+        if on != steady["on"]:
+            torch.cuda.set_sync_debug_mode("error" if on else "default")
+            steady["on"] = on
+    agent.learn(timesteps=timesteps, on_vector_step=on_step)
+    torch.cuda.set_sync_debug_mode("default")
+    assert steady["n"] > 20 and steady["checks"] == 0, steady
     # crossings of the timed loop: every vector step once training is ready
     ts = np.array([t for t, _ in agent.test_scores])
     sc = torch.tensor([s for _, s in agent.test_scores], dtype=torch.float64)
@@ -74,7 +98,7 @@ def main():
         best = float(sc.max())
         chk.load(os.path.join(tmp, "net_best.pth"))
         i_best = int(np.argmax(sc.numpy()))  # first occurrence = the evaluation that saved _best
-        test._eval_next_graph = (i_best * 10) % 10
+        test._eval_next_graph = (i_best * 10) % 25
         again, _ = chk.evaluate_agent()
         assert again == best, (again, best)
         print("EVAL_OK", len(ts), counts, best, flush=True)

@@ -367,32 +367,38 @@ def test_learn_evaluates_saves_and_pickles(tmp_path):
 
 def test_overlapped_evaluation_matches_synchronous(tmp_path):
     """learn() runs its one-fill evaluations on a side stream on a snapshot of the weights while training goes on
-    (DQN.overlap_evaluation, default on).  Against the same run with synchronous evaluate_agent() calls: the same
-    test scores and solutions at the same timesteps, the same `_best` network file, the same training losses."""
+    (DQN.overlap_evaluation, default on), each evaluation after the first replaying its rollout from a HIP graph
+    (DQN.eval_graphs).  Against the same run with synchronous, eagerly launched evaluate_agent() calls: the same
+    test scores and solutions at the same timesteps, the same `_best` network file, the same training losses; and
+    likewise for synchronous calls that replay the graph."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.agents.dqn.utils import TestMetric
     n, B = 20, 64
     out = []
-    for overlap in (False, True):
+    for overlap, graphs in ((False, False), (True, True), (False, True)):
         store = GraphStore.random("ER", 256, n, 0.15, seed=4)
         test_env = VecSpinSystem(GraphStore.random("ER", 8, n, 0.15, seed=5), 8, 2 * n,
                                  **{k: v for k, v in _dqn_for(store, n, B=B).env.env_args.items()})
-        d = tmp_path / str(overlap)
+        d = tmp_path / f"{overlap}_{graphs}"
         d.mkdir()
         agent = _dqn_for(store, n, B=B, replay_start_size=2 * B, train_minibatch=64, evaluate=True,
                          test_envs=test_env, test_episodes=8, test_frequency=B * 5, test_metric=TestMetric.BEST,
                          save_network_frequency=B * 1000, network_save_path=str(d / "network.pth"),
                          test_save_path=None, overlap_evaluation=overlap)
+        agent.eval_graphs = graphs
         assert agent._one_fill_ok(test_env, None)
         losses = agent.learn(timesteps=B * 41)
         best = torch.load(d / "network_best.pth", map_location="cpu", weights_only=True)
-        out.append((agent.test_scores, agent.test_solutions, losses, best, agent._eval_net is not None))
-    (s0, o0, l0, b0, e0), (s1, o1, l1, b1, e1) = out
-    assert not e0 and e1  # the second run did overlap
+        replayed = sum(r["graph"] is not None for r in agent._eval_graphs.values())
+        out.append((agent.test_scores, agent.test_solutions, losses, best, agent._eval_net is not None, replayed))
+    (s0, o0, l0, b0, e0, g0), (s1, o1, l1, b1, e1, g1), (s2, o2, l2, b2, e2, g2) = out
+    assert not e0 and e1 and not e2  # the second run did overlap
+    assert g0 == 0 and g1 == 1 and g2 == 1  # the eager run captured nothing; the others replayed a HIP graph
     assert [t for t, _ in s0] == [B * k for k in range(5, 41, 5)]
-    assert s0 == s1 and o0 == o1 and l0 == l1
-    assert all(torch.equal(b0[k], b1[k]) for k in b0)
+    # eager launches, the overlapped graph replay and the synchronous graph replay: identical scores, _best, losses
+    assert s0 == s1 == s2 and o0 == o1 == o2 and l0 == l1 == l2
+    assert all(torch.equal(b0[k], b1[k]) and torch.equal(b0[k], b2[k]) for k in b0)
 
 
 @pytest.mark.parametrize("n,B,basis,kind", [(20, 64, "SIGNED", "ER"), (200, 16, "BINARY", "ER"),
@@ -516,7 +522,7 @@ def test_evaluation_on_the_regenerated_training_store_is_synchronous(tmp_path):
     out = []
     for overlap in (False, True):
         st = GraphStore.slots(graph_slots_needed(B, T, C), n, edge_cap("ER", n, 0.15))
-        d = tmp_path / str(overlap)
+        d = tmp_path / f"{overlap}_{graphs}"
         d.mkdir()
         agent = _dqn_for(st, n, B=B, replay_buffer_size=C, replay_start_size=2 * B, train_minibatch=64,
                          regenerate_graphs=("ER", 0.15), evaluate=True, test_envs=None, test_episodes=8,

@@ -61,8 +61,9 @@ def test_two_ranks_train_to_identical_parameters():
 def test_two_ranks_evaluate_once_per_crossing():
     """learn() with evaluations at two ranks, every vector step crossing a test point (B x world > test_frequency,
     configs[3]'s regime at 8 GPUs): exactly one evaluation per crossing for the job, dealt round-robin to the ranks,
-    the same test scores recorded on every rank, and the `_best` checkpoint reproducing the best score
-    (dist_eval_worker.py)."""
+    the same test scores recorded on every rank, the `_best` checkpoint reproducing the best score, and no host
+    synchronisation in learn()'s steady state (torch sync-debug mode "error", no eco_check_errors call;
+    dist_eval_worker.py)."""
     outs = _run_ranks("dist_eval_worker.py", 2)
     line = next(l for l in outs[0].splitlines() if l.startswith("EVAL_OK"))
     assert int(line.split()[1]) > 4

@@ -1,11 +1,15 @@
 """The fp16x2 operand split of the dense kernels (split2_pk, eco_mpnn_dense2.h) emits v_fma_mix{lo,hi}_f16 as inline
 asm with its own trailing wait states: the compiler's hazard recognizer cannot see inside asm, and an MFMA that
 reads a VGPR written by VALU needs them (round 4: without them the paired and single forwards differed in the last
-bits).  eco_probe_split2_mfma runs the split inside an MFMA chain as the dense kernels' mm_fh does (order 0) and with
-the lo fragment consumed first, straight after the asm (order 1), beside the same products from a plain-conversion
-split (cvt / subtract / cvt): the accumulators must be bitwise equal for random activations, weights and scales.
-The negative control -- the same probe built without the wait states (ECO_SPLIT2_NEGATIVE_CONTROL, tools/
-r05_split2_negative.sh) -- is recorded in profiles/r05/split2_negative_control.log."""
+bits).  eco_probe_split2_mfma runs the split inside an MFMA chain as the dense kernels' mm_fh does (order 0), with
+the lo fragment consumed first, straight after the asm (order 1), and -- the discriminating case -- with the split's
+eight v_fma_mix and the first MFMA reading its lo fragment in ONE asm block built from the product's own asm text and
+wait states (ECO_MIXLO / ECO_MIXHI / ECO_SPLIT2_WAIT), so the MFMA reads the register the last v_fma_mixhi wrote
+with only those wait states between them (order 2; in orders 0 / 1 the compiler may place other instructions
+there).  Each beside the same products from a plain-conversion split (cvt / subtract / cvt): the accumulators must
+be bitwise equal for random activations, weights and scales.  The negative control -- the library built without the
+wait states (ECO_SPLIT2_NEGATIVE_CONTROL, tools/r06/split2_negative.sh) -- must fail order 2; its log is
+profiles/r06/split2_negative_control.log."""
 import ctypes
 
 import numpy as np
@@ -15,7 +19,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("order", [0, 1, 2])
 def test_split2_asm_matches_plain_split_inside_mfma_chain(order):
     from eco_hip import _lib
     rng = np.random.default_rng(order)
