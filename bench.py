@@ -553,9 +553,11 @@ def process_group_info(world, per_rank_s, steps, local, device):
 
 
 TARGET_SYNC_GRAD_STEPS = 16
+REPLAY_EPISODES = 1.0     # replay ring in episode batches of B x T transitions
+STAGGER_EPISODES = False  # DQN.stagger_episodes: episodes spread over the T phases of an episode
 
 
-def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=1.0,
+def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=None,
                       n_graphs=None, regenerate=True):
     """The benched configs[2] / configs[3] agent: B episodes on a pool of B seeded graphs (one per episode),
     experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377) batched, with the large-batch recipe of
@@ -579,7 +581,7 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     from eco_hip.networks.mpnn import MPNN
     from eco_hip.agents.dqn.dqn import DQN, graph_slots_needed
     T = 2 * n
-    cap = int(B * T * replay_episodes)
+    cap = int(B * T * (REPLAY_EPISODES if replay_episodes is None else replay_episodes))
     if regenerate:
         store = GraphStore.generated(graph, graph_slots_needed(B, T, cap), n, gparam, seed=seed, device=dev)
     else:
@@ -600,6 +602,7 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     # single-attempt 0.989 (nine seeds) against 0.983 at 125, BA-200 1.010 against 1.012; one copy of the parameter
     # vector, no throughput cost
     agent.target_sync_grad_steps = TARGET_SYNC_GRAD_STEPS
+    agent.stagger_episodes = STAGGER_EPISODES
     return agent, store, env, lr
 
 

@@ -192,6 +192,9 @@ class DQN:
         # (env, network) pair (_capture_eval_rollout); False keeps every evaluation's launches eager
         self.eval_graphs = True
         self._eval_graphs = {}
+        # learn(): spread the B lockstep episodes over the T phases of an episode (start(); False: all B episodes
+        # start together and end together every T vector steps)
+        self.stagger_episodes = False
 
         self._act_counter = 0
         self._alloc_train_buffers(self.M)
@@ -376,6 +379,7 @@ class DQN:
         else:
             m = np.asarray(mask.cpu() if torch.is_tensor(mask) else mask).astype(bool)
             self._host_graph_ids[m] = ids[m]
+            mask = self.env._upload(mask, torch.uint8)  # one non-blocking upload for the env and the replay
         self.env.reset(graph_ids=graph_ids, mask=mask, seed=seed)
         if self.compact_replay:
             self.replay_buffer.snapshot(mask)
@@ -401,6 +405,14 @@ class DQN:
         # every episode ends exactly at max_steps only for reversible spins with Stopping.NORMAL
         # (spinsystem.py:539-554); otherwise dones are read back after each vector step
         self._lockstep = self.env.reversible_spins and self.env.cfg.stopping == 1
+        # staggered episodes (stagger_episodes, lockstep envs only): episode b's first episode is cut after
+        # T - (b T // B) steps (its last transition stored with the env's done = 0: a truncation, not a terminal),
+        # so from then on the B episodes sit at B / T evenly spread phases and ~B / T of them end and are reset on
+        # fresh graphs every vector step, as a single reference env's consecutive episodes pass through every phase
+        self._stagger = bool(self.stagger_episodes and self._lockstep)
+        if self._stagger:
+            T = self.env.max_steps
+            self._ep_left = T - (np.arange(self.B, dtype=np.int64) * T) // self.B
 
     def iteration(self):
         """One vector step of DQN.learn (dqn.py:273-347): act/step/add for all B episodes, reset
@@ -418,7 +430,13 @@ class DQN:
             self.update_epsilon(self._timestep - 1)
         if self.update_learning_rate:
             self.update_lr(self._timestep - 1)
-        if self._lockstep:
+        if self._stagger:
+            self._ep_left -= 1
+            ending = self._ep_left == 0
+            if ending.any():
+                self._reset_env(self._take_graph_slots(ending), self.seed + self._timestep, mask=ending)
+                self._ep_left[ending] = T
+        elif self._lockstep:
             if self._steps_in_episode == T:
                 self._reset_env(self._take_graph_slots(None), self.seed + self._timestep)
                 self._steps_in_episode = 0

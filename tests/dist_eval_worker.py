@@ -51,6 +51,24 @@ def main():
     # device synchronisation (item(), cpu(), blocking copies, stream / device synchronize) from the 4th vector
     # step after training is ready (the first evaluation of each rank has captured its rollout graph by then)
     # to the last one, and the device error check (eco_check_errors) must not be called meanwhile
+    # gloo stages a CUDA tensor's all-reduce through the host on its own thread (a synchronisation the nccl backend
+    # does not have: RCCL runs on its own stream and work.wait() only orders the streams), so this gloo rehearsal
+    # runs the per-gradient-step exchange to completion with the check off; everything else learn() does is checked
+    import eco_hip.agents.dqn.dqn as dqn_mod
+    real_allreduce = dqn_mod.allreduce_gradients_async
+
+    def allreduce_exempt(grad, group=None):
+        mode = torch.cuda.get_sync_debug_mode()
+        torch.cuda.set_sync_debug_mode(0)
+        try:
+            work, scale = real_allreduce(grad, group)
+            if work is not None:
+                work.wait()
+            torch.cuda.synchronize()
+        finally:
+            torch.cuda.set_sync_debug_mode(mode)
+        return None, scale
+    dqn_mod.allreduce_gradients_async = allreduce_exempt
     steady = {"n": 0, "on": False, "checks": 0}
     real_check = agent.graphs.check_errors
 

@@ -50,9 +50,10 @@ def family_graphs(kind, n, seed):
     return [og.ba_graph(n, 4, rng) for _ in range(N_GRAPHS)]
 
 
-def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048, configure=None):
+def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048, configure=None, replay_episodes=None):
     """The benched agent trained by learn(); returns (the `_best` network, info).  configure: optional callable on
-    the agent before training (tools/r05/quality_sweep.py)."""
+    the agent before training (tools/r06/quality_sweep.py); replay_episodes: the replay ring in episode batches of
+    B x T transitions (default: bench.REPLAY_EPISODES, the benched ring)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
     from eco_hip.networks.mpnn import MPNN
@@ -60,7 +61,9 @@ def train_and_select(kind, param, n, seed, steps=10_000_000, B=8192, M=2048, con
     sys.path.insert(0, REPO)
     import bench
     dev = torch.device("cuda", 0)
-    agent, _, env, lr = bench.build_train_agent(dev, B, n, kind, param, M, seed=seed)
+    agent, _, env, lr = bench.build_train_agent(dev, B, n, kind, param, M, seed=seed,
+                                                 **({} if replay_episodes is None else
+                                                    {"replay_episodes": replay_episodes}))
     val = VecSpinSystem(GraphStore.from_dense(family_graphs(kind, n, 9000 + (kind == "BA"))), 64, 2 * n,
                         **env.env_args)
     tmp = tempfile.mkdtemp(prefix=f"eco_quality_{kind}{n}_{seed}_")

@@ -522,7 +522,7 @@ def test_evaluation_on_the_regenerated_training_store_is_synchronous(tmp_path):
     out = []
     for overlap in (False, True):
         st = GraphStore.slots(graph_slots_needed(B, T, C), n, edge_cap("ER", n, 0.15))
-        d = tmp_path / f"{overlap}_{graphs}"
+        d = tmp_path / str(overlap)
         d.mkdir()
         agent = _dqn_for(st, n, B=B, replay_buffer_size=C, replay_start_size=2 * B, train_minibatch=64,
                          regenerate_graphs=("ER", 0.15), evaluate=True, test_envs=None, test_episodes=8,
@@ -588,3 +588,53 @@ def test_learn_with_staggered_dones_resets_only_finished_episodes():
     agent.learn(timesteps=B * 20)
     second = agent.losses()
     assert len(second) == agent.grad_steps - n1 > 0
+
+
+def test_stagger_episodes_spreads_phases_with_fresh_graphs():
+    """DQN.stagger_episodes on a lockstep env (reversible spins, Stopping.NORMAL): episode b's first episode is cut
+    after T - (b T // B) steps, then every episode runs the full T steps, so the B episodes sit at evenly spread
+    phases.  Checked every vector step against the env's own step counters: each episode's current step follows
+    that schedule, exactly the episodes whose counters wrap are reset (fresh graph slots with regenerate_graphs,
+    the others keep theirs), and training proceeds.  The truncated transition is not terminal: the env's done flag
+    is set only at max_steps, which the replay stores as it is (the steps before the truncation all read done 0)."""
+    from eco_hip.graphs import GraphStore
+    from eco_hip.envs.batched import VecSpinSystem
+    from eco_hip.envs.utils import (DEFAULT_OBSERVABLES, RewardSignal, ExtraAction, OptimisationTarget,
+                                    SpinBasis)
+    from eco_hip.networks.mpnn import MPNN
+    from eco_hip.agents.dqn.dqn import DQN, graph_slots_needed
+    n, B = 20, 64
+    T = 2 * n
+    cap = B * 8
+    store = GraphStore.generated("ER", graph_slots_needed(B, T, cap), n, 0.15, seed=5, device="cuda")
+    env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
+                        extra_action=ExtraAction.NONE, optimisation_target=OptimisationTarget.CUT,
+                        spin_basis=SpinBasis.SIGNED, norm_rewards=True, basin_reward=1. / n)
+    agent = DQN(env, lambda: MPNN(device="cuda"), init_weight_std=0.01, replay_start_size=2 * B,
+                replay_buffer_size=cap, gamma=0.95, update_target_frequency=1000, update_learning_rate=False,
+                initial_learning_rate=1e-4, peak_learning_rate=1e-4, final_learning_rate=1e-4, update_frequency=32,
+                minibatch_size=64, final_exploration_rate=0.05, final_exploration_step=20000, seed=21,
+                evaluate=False, test_save_path=None, regenerate_graphs=("ER", 0.15))
+    agent.stagger_episodes = True
+    first_len = T - (np.arange(B) * T) // B
+    k = {"v": 0}
+    prev = {}
+
+    def watch(t):
+        k["v"] += 1
+        kv = k["v"]
+        steps = agent.env.read()["current_step"].cpu().numpy().astype(np.int64)
+        gids = agent.env.graph_ids.cpu().numpy()
+        expect = np.where(kv < first_len, kv, (kv - first_len) % T)
+        np.testing.assert_array_equal(steps, expect)
+        if prev:
+            reset = expect == 0
+            np.testing.assert_array_equal(gids[~reset], prev["gids"][~reset])
+            assert not np.isin(gids[reset], prev["gids"]).any()  # fresh slots (none shared with live episodes)
+        prev["gids"] = gids
+
+    agent.learn(timesteps=B * 3 * T, on_vector_step=watch)
+    assert agent._stagger and agent.graphs_regenerated > 0
+    assert agent.grad_steps > 0 and torch.isfinite(agent.network.flat).all()
+    # phases are spread: after the first truncations every step resets B / T episodes
+    assert sorted(set(((k["v"] - first_len) % T).tolist())) == list(range(T))
