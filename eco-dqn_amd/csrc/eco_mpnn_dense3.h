@@ -36,20 +36,19 @@ constexpr int D3_NW = 8;  // waves per workgroup
 #define D3_LIN_SPLIT_AHEAD 1  // A/B: the inference forward's Linears split one step ahead
 #endif
 
-// LDS byte address of a plane element.  (Making it opaque -- one base register plus immediate offsets per
-// fragment read instead of the compiler's v_or of the lane part with a >16-bit constant -- removed ~220 VALU from
-// the kernel and measured no faster: 0.7007-0.703 vs 0.6976-0.6987 ms per M = 2048 launch, profiles/r05/.)
+// Transposed fragment reads of the planes through LDS pointers derived from the plane array itself (address-space
+// casts and element offsets), not integer byte addresses: the compiler's alias analysis then sees that they cannot
+// touch a weight buffer an LDS-DMA is filling, and does not make them wait for the DMA (an integer-built address --
+// round 5's opaque base, ~220 VALU fewer -- forced s_waitcnt vmcnt(0) before each layer's first plane reads, i.e.
+// waited for the next weights' DMA instead of landing it under the aggregation).
 typedef __attribute__((address_space(3))) v4s lds_v4s;
-__device__ __forceinline__ uint32_t lds_base(const uint16_t* p) {
-  return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
+__device__ __forceinline__ v4s tr_read_p(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
 }
-__device__ __forceinline__ v4s tr_read_at(uint32_t b, int bytes) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(size_t)(b + (uint32_t)bytes));
-}
-// the (lo, hi) fragment pair of plane base b, chunk kc, feature block ft (the lane part is in b)
-__device__ __forceinline__ f16x8 plane_frag(uint32_t b, int kc, int ft) {
-  const int o = 2 * (32 * kc * 16 + ft * (DN_KPMAX * 16));
-  const v4s lo = tr_read_at(b, o), hi = tr_read_at(b, o + 2 * 16 * 16);
+// the (lo, hi) fragment pair of plane base b (the lane part included), chunk kc, feature block ft
+__device__ __forceinline__ f16x8 plane_frag(const uint16_t* b, int kc, int ft) {
+  const int o = 32 * kc * 16 + ft * (DN_KPMAX * 16);
+  const v4s lo = tr_read_p(b + o), hi = tr_read_p(b + o + 16 * 16);
   const bf16x8 raw = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(f16x8, raw);
 }
@@ -70,7 +69,7 @@ __device__ __forceinline__ void agg3(f32x4 (&acc)[2][4], const uint16_t* P0, con
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;
-  const uint32_t pb[2] = {lds_base(P0 + j_in * 16 + 4 * pc), lds_base(P1 + j_in * 16 + 4 * pc)};
+  const uint16_t* pb[2] = {P0 + j_in * 16 + 4 * pc, P1 + j_in * 16 + 4 * pc};
 #pragma unroll
   for (int kc = 0; kc < DN_KC; ++kc) {
     if (kc < kc0 || kc >= kc1) continue;  // wave-uniform
@@ -106,7 +105,7 @@ __device__ __forceinline__ void agg3f(f32x4 (&acc)[2][4], const uint16_t* P0, co
   const int q = lane >> 4;
   const int j_in = 4 * q + ((lane >> 2) & 3);
   const int pc = (lane & 3) ^ q;
-  const uint32_t pb[2] = {lds_base(P0 + j_in * 16 + 4 * pc), lds_base(P1 + j_in * 16 + 4 * pc)};
+  const uint16_t* pb[2] = {P0 + j_in * 16 + 4 * pc, P1 + j_in * 16 + 4 * pc};
   f16x8 fa[2][8], fb[2][2];
   auto issue = [&](int kc, int buf) {
 #pragma unroll
@@ -260,20 +259,27 @@ if constexpr (AHEAD) {
 
 // The seven matrix scales kw (PK_FHS: Wf, then (Wm, Wu) per layer) as vector loads issued early; each use makes its
 // value wave-uniform (readfirstlane), so the load latency is waited for at the first use, not at the kernel start.
+// Seven separate members, not an array: with an array the per-layer select became a dynamically indexed private
+// array (scratch memory), whose store at the staging and load at the top of every layer each forced a vmcnt(0) --
+// waiting for every load and weight DMA in flight (the layer weights meant to land under the aggregation).
 struct KwLoad {
-  int v[FH_NMAT];
-  __device__ __forceinline__ explicit KwLoad(const float* P) {
-#pragma unroll
-    for (int m = 0; m < FH_NMAT; ++m) v[m] = fh_kw(P, m);
-  }
-  __device__ __forceinline__ int operator[](int m) const { return __builtin_amdgcn_readfirstlane(v[m]); }
-  __device__ __forceinline__ int message(int layer) const {
-    return __builtin_amdgcn_readfirstlane(layer == 0 ? v[1] : (layer == 1 ? v[3] : v[5]));
-  }
-  __device__ __forceinline__ int update(int layer) const {
-    return __builtin_amdgcn_readfirstlane(layer == 0 ? v[2] : (layer == 1 ? v[4] : v[6]));
+  int v0, v1, v2, v3, v4, v5, v6;  // as loaded (VGPRs, in flight until ECO_KW_SCALARS reads them)
+  __device__ __forceinline__ explicit KwLoad(const float* P)
+      : v0(fh_kw(P, 0)), v1(fh_kw(P, 1)), v2(fh_kw(P, 2)), v3(fh_kw(P, 3)), v4(fh_kw(P, 4)), v5(fh_kw(P, 5)),
+        v6(fh_kw(P, 6)) {
+    static_assert(FH_NMAT == 7, "one member per packed matrix scale");
   }
 };
+// The scales as wave-uniform scalars, read once the staging's loads have landed (after its vmcnt(0)): seven SGPRs
+// instead of seven VGPRs live through the layers (the paired kernel spilled with them), selected per layer from
+// separate values (kept out of any array, which the compiler would index in scratch memory)
+#define ECO_KW_SCALARS(kw)                                                                                  \
+  const int kw_f = __builtin_amdgcn_readfirstlane((kw).v0), kw_m0 = __builtin_amdgcn_readfirstlane((kw).v1), \
+            kw_u0 = __builtin_amdgcn_readfirstlane((kw).v2), kw_m1 = __builtin_amdgcn_readfirstlane((kw).v3), \
+            kw_u1 = __builtin_amdgcn_readfirstlane((kw).v4), kw_m2 = __builtin_amdgcn_readfirstlane((kw).v5), \
+            kw_u2 = __builtin_amdgcn_readfirstlane((kw).v6)
+#define ECO_KW_MESSAGE(layer) ((layer) == 0 ? kw_m0 : ((layer) == 1 ? kw_m1 : kw_m2))
+#define ECO_KW_UPDATE(layer) ((layer) == 0 ? kw_u0 : ((layer) == 1 ? kw_u1 : kw_u2))
 
 __device__ __forceinline__ void zero_acc2(f32x4 (&d)[2][4]) {
 #pragma unroll
@@ -454,6 +460,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   lds_barrier();
   D3_PRIO(3);
   ECO_TS(2);
+  ECO_KW_SCALARS(kw);
   if (first) {  // the staged adjacency and degrees, first needed here
     d3_spread(adjb, valid, adjw);
 #pragma unroll
@@ -504,7 +511,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     mm_fh_2t(d, acc[0], acc[1], sfx, WB0, lane);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      unscale(d[t], kx[t] + kw[0]);
+      unscale(d[t], kx[t] + kw_f);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         ereg[t][nt] = relu4(d[t][nt]);
@@ -553,8 +560,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   for (int layer = 0; layer < 3; ++layer) {
     const uint16_t* WM = layer == 0 ? WB1 : (layer == 1 ? WB0 : WB2);
     const uint16_t* WU = layer == 0 ? WB2 : (layer == 1 ? WB1 : WB0);
-    const int kwm = kw.message(layer);  // wave-uniform selects (a runtime index put kw[] in scratch memory)
-    const int kwu = kw.update(layer);
+    const int kwm = ECO_KW_MESSAGE(layer);  // scalar selects (KwLoad)
+    const int kwu = ECO_KW_UPDATE(layer);
     if (layer == 1) {
       glds_frags<NW>(WB1, PH + FH_LAYER + FH_LAYER_STRIDE + 2 * FH_HALF, 32, w, lane);  // Wu1
       glds_frags<NW>(WB2, PH + FH_LAYER + 2 * FH_LAYER_STRIDE, 32, w, lane);            // Wm2
@@ -1000,6 +1007,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   }
   glds_wait();     // Wu^T / Wm^T of layer 2 and Wu^T of layer 1 (staged at the start) are read from here on
   lds_barrier();  // readout scratch dead: zero the plane rows [rows_pad, KP) no tile writes
+  ECO_KW_SCALARS(kw);
   zero_pad_rows2<NT>(PL, PL1, rows_pad);
   // the staged adjacency and degrees, first needed by the layers (their loads ran under the readout backward)
   d3_spread(adjb, valid, adjw);
@@ -1019,8 +1027,8 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
   for (int layer = 2; layer >= 0; --layer) {
     const uint16_t* WU = layer == 2 ? WB0 : (layer == 1 ? WB2 : WB1);
     const uint16_t* WM = layer == 2 ? WB1 : (layer == 1 ? WB0 : WB2);
-    const int kwm = kw.message(layer);
-    const int kwu = kw.update(layer);
+    const int kwm = ECO_KW_MESSAGE(layer);
+    const int kwu = ECO_KW_UPDATE(layer);
     // duu = dh' * [h' > 0]  (in place in dh)
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1168,7 +1176,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_backward_dense3_kernel(Mpn
     mm_fh_2t(dg, due[0], due[1], sf, WB0, lane);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      unscale(dg[t], kx[t] + kw[0]);
+      unscale(dg[t], kx[t] + kw_f);
       float4 g[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
