@@ -413,6 +413,14 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   ECO_TS(1);
   float rnf[2];
   // aggregation chunks of the wave's rows (the union of its two tiles' ranges)
+  // a tile row recomputed from a laundered lane id where it is used after the staging, so the compiler does not keep
+  // r[] live through the layers (the paired kernel spilled it and reloaded it with vmcnt(0), i.e. waiting for the
+  // weight DMA in flight)
+  auto row_of = [&](int t) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    return tl[t] * 16 + (ln & 15);
+  };
   const int g_lo = min(w * 32, rows_pad - 1) / N, g_hi = min(w * 32 + 31, rows_pad - 1) / N;
   const int kc0 = (g_lo * N) >> 5;
   const int kc1 = (min((g_hi + 1) * N, rows_pad) + 31) >> 5;
@@ -543,7 +551,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
         if (SAVE && valid[t])
           st4(a.sv + (size_t)SV_H0 * RT * 64 + (R0 + r[t]) * 64 + 16 * c + 4 * s4, hreg[t][c]);
       }
-      if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
+      if (has[t]) tile_planes(PL, PL1, TE, tl[t], row_of(t), s4, hreg[t], lane);
       if (SAVE && valid[t]) store_mask(a, RT, R0 + r[t], s4, SM_H0, pos_mask(hreg[t]));
     }
   } else {
@@ -660,7 +668,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
     if (layer < 2) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        if (has[t]) tile_planes(PL, PL1, TE, tl[t], r[t], s4, hreg[t], lane);
+        if (has[t]) tile_planes(PL, PL1, TE, tl[t], row_of(t), s4, hreg[t], lane);
     }
     D3_PRIO(0);
     if (layer == 0) ECO_TS(14);
@@ -695,7 +703,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
       ql = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
       auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ql), __float_as_uint(ql), false, false);
       ql = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
-      if (s4 == 0) QL[r[t]] = ql;
+      if (s4 == 0) QL[row_of(t)] = ql;
       float cs[16];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -761,7 +769,7 @@ __global__ __launch_bounds__(64 * D3_NW, 1) void mpnn_forward_dense3_kernel(Mpnn
   for (int t = 0; t < 2; ++t) {
     if (!has[t]) continue;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) st4(Hs + r[t] * D2_HS_LD + 16 * c + 4 * s4, hreg[t][c]);
+    for (int c = 0; c < 4; ++c) st4(Hs + row_of(t) * D2_HS_LD + 16 * c + 4 * s4, hreg[t][c]);
   }
   lds_barrier();
   float* Scr = reinterpret_cast<float*>(sW1);
