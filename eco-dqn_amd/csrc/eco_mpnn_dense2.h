@@ -213,7 +213,12 @@ __device__ __forceinline__ void unscale(f32x4 (&acc)[4], int k) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[nt][i] = __builtin_ldexpf(acc[nt][i], -k);
 }
-__device__ __forceinline__ int fh_kw(const float* P, int m) { return __float_as_int(P[PK_FHS + m]); }
+// scale exponent of packed matrix m: a SCALAR load through the constant address space (P and m are uniform, the
+// packed parameters are read-only during every kernel), so its wait is lgkmcnt and never vmcnt -- a vector load
+// here, used right away, made the wave wait for every older vector load and weight DMA in flight
+__device__ __forceinline__ int fh_kw(const float* P, int m) {
+  return ((const __attribute__((address_space(4))) int*)(P + PK_FHS))[m];
+}
 
 // ---- planes ---------------------------------------------------------------------------------------------------
 // tile scale exponent of the wave's 16 nodes x 64 features (identical in every lane; D2_K_EMPTY for all zero)

@@ -346,6 +346,12 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_forward_dl_kernel(MpnnArgs
   }
   ECO_TS(4);
 
+  // the lane's row offset of tile i, recomputed from a laundered lane id inside the layer loop (see the backward)
+  auto ro_of = [&](int i) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    return (R0 + (size_t)((w + NW * i) * 16 + (ln & 15))) * 64 + 4 * (ln >> 4);
+  };
   // ---- phase D: 3 x UpdateNodeEmbeddingLayer (mpnn.py:114-120); Wm in sW0, Wu in sW1 ----
 #pragma unroll 1
   for (int layer = 0; layer < 3; ++layer) {
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_forward_dl_kernel(MpnnArgs
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       if (i >= ntw) break;
-      const size_t ro = (R0 + rI[i]) * 64 + 4 * s4;
+      const size_t ro = ro_of(i);
       float4 e[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) e[c] = vI[i] ? f4(ev + ro + 16 * c) : zero4();
@@ -659,6 +665,13 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_backward_dl_kernel(MpnnArg
   dl_zero_pad<NT>(PL0, PL1, rows_pad);
   ECO_TS(18);
 
+  // the lane's row offset of tile i, recomputed from a laundered lane id inside the layer loop: hoisted out of it,
+  // the per-tile row addresses stayed live through every layer and were spilled (scratch reloads wait for vmcnt(0))
+  auto ro_of = [&](int i) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    return (R0 + (size_t)((w + NW * i) * 16 + (ln & 15))) * 64 + 4 * (ln >> 4);
+  };
   // ---- update layers in reverse (mpnn.py:114-120) ----
 #pragma unroll 1
   for (int layer = 2; layer >= 0; --layer) {
@@ -669,7 +682,7 @@ __global__ __launch_bounds__(64 * DL_NW, 1) void mpnn_backward_dl_kernel(MpnnArg
       tg[i] = D2_K_EMPTY;
       ghi[i][0] = ghi[i][1] = zero4();
       if (i >= ntw) continue;
-      const size_t ro = (R0 + rI[i]) * 64 + 4 * s4;
+      const size_t ro = ro_of(i);
       // duu = dh' * [h' > 0]
       float4 duu[4];
       {
