@@ -4,7 +4,7 @@ the CSR-gather kernels (eco_mpnn.hip) on the same inputs, and against the fp32 t
 The CSR path is selected per call with the ECO_PATH_NO_DENSE kernel-path bit (eco_set_kernel_paths).  Both compute the reference's fp32
 arithmetic in a different summation order (dense: exact bf16x3 splits, fp32 accumulation), so the bars
 are the oracle tolerances of test_mpnn_gpu / test_dqn_gpu:
-  Q: |q - q_ref| <= 5e-5 (1 + |q_ref|);  gradients: relative L2 error < 2e-4 per parameter tensor against
+  Q: |q - q_ref| <= 5e-7 (1 + |q_ref|) (measured <= 6.3e-8, profiles/r06/numerics_errors.log);  gradients: relative L2 error < 1e-5 (measured <= 1.3e-6) per parameter tensor against
   float64 autograd of the oracle.
 Covers one graph per block with the prepared bitmask (N = 150, 200, 224), one graph per block built
 in-kernel (adjbits dropped), several graphs per block (N = 20, 64), padding rows, and the fallback for
@@ -49,7 +49,9 @@ def _run(net, store, x, dq, scope, dense):
 
 
 def _scaled_err(a, b):
-    return float(((a - b).abs() / (1 + b.abs())).max())
+    e = float(((a - b).abs() / (1 + b.abs())).max())
+    print(f"scaled err {e:.3e}")
+    return e
 
 
 @pytest.mark.parametrize("n,B,prepared", [(200, 24, True), (224, 9, True), (150, 16, True), (200, 10, False),
@@ -68,10 +70,10 @@ def test_dense_matches_csr_and_oracle(n, B, prepared):
     qd, qsd, gd = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=True)
     qc, qsc, gc = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=False)
     assert torch.isfinite(qd).all() and torch.isfinite(gd).all()
-    assert _scaled_err(qd, qc) <= 5e-5 and _scaled_err(qsd, qsc) <= 5e-5
+    assert _scaled_err(qd, qc) <= 5e-7 and _scaled_err(qsd, qsc) <= 5e-7
     for b in [0, B // 2, B - 1]:  # oracle, per-graph norm scope (B=1 semantics)
         obs = torch.from_numpy(np.vstack([x[b, :, :7].cpu().numpy().T.astype(np.float64), store.dense(b)])).float()
-        assert _scaled_err(qd[b], mo.forward(w, obs)) <= 5e-5
+        assert _scaled_err(qd[b], mo.forward(w, obs)) <= 5e-7
     # gradients: dense vs torch autograd of the oracle (norm.max over the batch, as train_step) evaluated in
     # float64.  The fp32 oracle is not the judge here: a ReLU input within fp32 rounding of 0 takes either
     # side depending on the summation order, and at N=20 the fp32 oracle's own edge-embedding gradients sit
@@ -84,7 +86,8 @@ def test_dense_matches_csr_and_oracle(n, B, prepared):
     for k in mo.KEYS:
         ref = w64[k].grad
         err = float((dd[k].double() - ref).norm() / max(float(ref.norm()), 1e-12))
-        assert err < 2e-4, (k, err)
+        print(f"grad {k} rel L2 vs float64 {err:.3e}")
+        assert err < 1e-5, (k, err)
         # CSR path: same math, other summation order (a ReLU input within rounding of 0 may take the other
         # side), so this cross-check only catches gross errors
         err_c = float((dd[k] - dc[k]).norm() / max(float(dc[k].norm()), 1e-12))
@@ -114,7 +117,7 @@ def test_non_unit_weights_use_the_csr_path():
     q = net.forward_graphs(x.cuda(), store, gids).cpu()
     for b in range(B):
         obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), mats[b]])).float()
-        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-5
+        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-7
 
 
 @pytest.mark.parametrize("n,B,kind,param", [(500, 6, "BA", 4), (512, 3, "BA", 4), (497, 3, "BA", 4),
@@ -131,20 +134,21 @@ def test_dense_large_matches_csr_and_oracle(n, B, kind, param):
     qc, qsc, gc = _run(net, store, x, dq, ECO_NORM_PER_GRAPH, dense=False)
     assert torch.isfinite(qd).all() and torch.isfinite(gd).all()
     assert not torch.equal(qd, qc)  # two different kernels ran
-    assert _scaled_err(qd, qc) <= 5e-5 and _scaled_err(qsd, qsc) <= 5e-5
+    assert _scaled_err(qd, qc) <= 5e-7 and _scaled_err(qsd, qsc) <= 5e-7
     wc = {k: v.cuda() for k, v in w.items()}
     obs = torch.stack([torch.from_numpy(np.vstack([x[b, :, :7].cpu().numpy().T.astype(np.float64), store.dense(b)]))
                        for b in range(B)]).cuda()
     with torch.no_grad():
         for b in range(B):
-            assert _scaled_err(qd[b], mo.forward(wc, obs[b].float()).cpu()) <= 5e-5, b
+            assert _scaled_err(qd[b], mo.forward(wc, obs[b].float()).cpu()) <= 5e-7, b
     w64 = {k: v.cuda().double().clone().requires_grad_(True) for k, v in w.items()}
     (mo.forward(w64, obs) * dq.double()).sum().backward()
     dd, dc = _flat_to_dict(gd), _flat_to_dict(gc)
     for k in mo.KEYS:
         ref = w64[k].grad.cpu()
         err = float((dd[k].double() - ref).norm() / max(float(ref.norm()), 1e-12))
-        assert err < 2e-4, (k, err)
+        print(f"grad {k} rel L2 vs float64 {err:.3e}")
+        assert err < 1e-5, (k, err)
         err_c = float((dd[k] - dc[k]).norm() / max(float(dc[k].norm()), 1e-12))
         assert err_c < 2e-2, (k, err_c)
     # fused greedy act on the dense kernel (per-call norm scope)

@@ -1,7 +1,7 @@
 """Every bit of the MPNN kernel-path policy (eco_set_kernel_paths, include/eco_hip.h) routes a call to
 another product kernel family; each routed call must give the default path's results within the fp32
 bars of the other MPNN tests (the same forward of mpnn.py:40-159 in a different summation order):
-  Q: |q - q_default| <= 5e-5 (1 + |q_default|);  gradients: relative L2 difference < 2e-4 per tensor.
+  Q: |q - q_default| <= 5e-7 (1 + |q_default|) (measured <= 6.2e-8);  gradients: relative L2 difference < 5e-6 per tensor.
 NO_DENSE is covered against the dense kernels in test_dense_gpu.py; here NO_DL (BA one-graph blocks of
 224 < N <= 512 on the CSR-gather kernels), NO_SHARED (one shared graph of N > 512 on the per-episode
 global-memory kernel) and NO_PAIR / NO_DENSE on the double-DQN pair (two eco_mpnn_forward calls, bitwise
@@ -33,11 +33,15 @@ def _x(B, n, seed):
 
 
 def _scaled(a, b):
-    return float(((a - b).abs() / (1 + b.abs())).max())
+    e = float(((a - b).abs() / (1 + b.abs())).max())
+    print(f"scaled err {e:.3e}")
+    return e
 
 
 def _rel(a, b):
-    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+    e = float((a - b).norm() / b.norm().clamp_min(1e-30))
+    print(f"rel L2 {e:.3e}")
+    return e
 
 
 def test_no_dl_matches_dense_large_kernels():
@@ -62,13 +66,13 @@ def test_no_dl_matches_dense_large_kernels():
             torch.cuda.synchronize()
             out[mask] = (q, qs, grad.clone())
     (q0, qs0, g0), (q1, qs1, g1) = out[0], out[_lib.ECO_PATH_NO_DL]
-    assert _scaled(q1, q0) <= 5e-5
-    assert _scaled(qs1, qs0) <= 5e-5
+    assert _scaled(q1, q0) <= 5e-7
+    assert _scaled(qs1, qs0) <= 5e-7
     from eco_hip.networks.mpnn import param_layout
     off = 0
     for name, shape in param_layout():
         k = int(np.prod(shape))
-        assert _rel(g1[off:off + k], g0[off:off + k]) < 2e-4, name
+        assert _rel(g1[off:off + k], g0[off:off + k]) < 5e-6, name
         off += k
 
 
@@ -93,7 +97,7 @@ def test_no_shared_matches_shared_graph_kernels():
             torch.cuda.synchronize()
             res[mask] = (q, a)
     (q0, a0), (q1, a1) = res[0], res[_lib.ECO_PATH_NO_SHARED]
-    assert _scaled(q1, q0) <= 5e-5
+    assert _scaled(q1, q0) <= 5e-7
     assert torch.equal(a0.long(), q0.argmax(1)) and torch.equal(a1.long(), q1.argmax(1))
 
 
@@ -123,7 +127,7 @@ def test_pair_paths(bit):
     if bit == "NO_PAIR":
         assert torch.equal(a0, a1) and torch.equal(q0, q1)
     else:
-        assert _scaled(q1, q0) <= 5e-5
+        assert _scaled(q1, q0) <= 5e-7
         qa = net.forward_graphs(x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL)
         assert torch.equal(a0.long(), qa.argmax(1))
 

@@ -2,7 +2,7 @@
 (mpnn_forward_large_kernel) against the fp32 torch oracle, the batched env at N = 2000 against the CPU
 oracle, and the boundary errors of the inference-only large path.
 
-Bars: Q within 5e-5 (1 + |q|) of the oracle (f32, other summation order); env rewards / spins bit-exact.
+Bars: Q within 5e-7 (1 + |q|) (measured <= 6.1e-8) of the oracle (f32, other summation order); env rewards / spins bit-exact.
 G22 itself is absent from the reference (.MISSING_LARGE_BLOBS:1): a seeded ER(N, p) graph with unit
 weights stands in (G22 is an unweighted 2000-vertex, 19,990-edge random graph)."""
 import numpy as np
@@ -17,7 +17,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _scaled_err(a, b):
-    return float(((a - b).abs() / (1 + b.abs())).max())
+    e = float(((a - b).abs() / (1 + b.abs())).max())
+    print(f"scaled err {e:.3e}")
+    return e
 
 
 @pytest.mark.parametrize("n,B,p", [(600, 3, 0.02), (1000, 2, 0.01)])
@@ -38,7 +40,7 @@ def test_large_forward_matches_oracle(n, B, p):
     q = net.forward_graphs(x.cuda(), store, gids, norm_scope=ECO_NORM_PER_GRAPH).cpu()
     for b in range(B):
         obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), mats[b]])).float()
-        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-5
+        assert _scaled_err(q[b], mo.forward(w, obs)) <= 5e-7
     # per-call norm scope + fused greedy act = argmax of the returned Q
     acts = torch.empty(B, dtype=torch.int32, device="cuda")
     qc = torch.empty(B, n, device="cuda")

@@ -2,8 +2,10 @@
 (tests/golden/mpnn_fwd.npz, produced by the reference itself) and with the fp32
 torch oracle (oracle/mpnn_oracle.py) at batch scale.
 
-Tolerance (floating point, fp32): |q - q_ref| <= 2e-5 * (1 + |q_ref|)  -- the
-kernels use exact-f32 MFMA but a different summation order than torch CPU.
+Tolerance (floating point, fp32): |q - q_ref| <= 5e-7 * (1 + |q_ref|).  The kernels compute with 22-bit
+fp16x2 operand splits and f32 accumulation in another summation order than torch CPU; measured round 6
+(profiles/r06/numerics_errors.log): at most 6.7e-8, i.e. fp32 rounding level, so the bar leaves ~7x headroom
+(it was 2e-5 / 5e-5 before round 6).
 """
 import os
 
@@ -15,13 +17,14 @@ from conftest import GOLDEN
 from oracle import mpnn_oracle as mo
 
 pytestmark = pytest.mark.gpu
-RTOL = 2e-5
+RTOL = 5e-7
 
 
 def _close(q, ref, tol=RTOL):
     q = np.asarray(q, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     err = np.abs(q - ref) / (1.0 + np.abs(ref))
+    print(f"max scaled err {err.max():.3e} (bar {tol:.0e})")
     assert err.max() <= tol, f"max scaled err {err.max():.3e}"
 
 
@@ -96,7 +99,7 @@ def test_forward_matches_oracle_at_scale(n, B):
         J = store.dense(b)
         obs = torch.from_numpy(np.vstack([x[b, :, :7].numpy().T.astype(np.float64), J])).float()
         ref = mo.forward(w, obs).numpy()
-        _close(q[b], ref, tol=5e-5)
+        _close(q[b], ref)
 
 
 def test_fused_act_greedy_and_epsilon():
