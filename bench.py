@@ -197,8 +197,8 @@ def cpu_refcost_baseline(n=200, seconds=10.0, gpus_on_node=1):
                 calibration_ratio_vs_reference=cal)
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r05", "final", "train", "pmc_hbm.json")
-PMC_SQ = os.path.join(REPO, "profiles", "r05", "final", "train", "pmc_sq_dense.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r06", "final", "train", "pmc_hbm.json")
+PMC_SQ = os.path.join(REPO, "profiles", "r06", "final", "train", "pmc_sq_dense.json")
 PMC_PAIRED = True  # the committed train PMC pass ran the paired s' forward (eco_mpnn_forward_pair)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA peak (~2.5 PF)
 
@@ -811,31 +811,69 @@ def inference_bench(args, world, rank, local, dev, dist):
     gids_np = np.arange(B) % ngraphs
     env.reset(graph_ids=gids_np, seed=seed)
     gids = env.graph_ids
+    gids_dev = gids.clone()
     acts = torch.empty(B, dtype=torch.int32, device=dev)
     greedy = _lib.ActConfig(0.0, 1, 0.0, 0, 0)
     timers = []
-    net.timer = timers
+    # configs[1]: an ER-20 episode is T = 40 steps of ~100 us of GPU work each, paced by the host's two launches per
+    # step; each whole episode is replayed from a HIP graph captured once (the same launches, as DQN's evaluation
+    # rollouts).  The forward's roofline is then timed with HIP events on one eager episode after the timed region
+    # (events cannot sit inside the graph).  configs[4] (T = 4000, ~2.6 ms per step) stays eager, timed live.
+    graphed = args.workload == "er20"
+    net.timer = None if graphed else timers
 
     # the episodes' graphs never change: the call's max degree (norm.max(), dqn.py:546-547) is computed by the
     # first forward and reused from the workspace after it (ECO_NORM_PER_CALL_REUSE: same values, one 1-workgroup
     # launch fewer per step)
     scope = [_lib.ECO_NORM_PER_CALL]
+    t_ep = [0]  # steps of the current episodes (all B episodes run in lockstep)
+    ep_seed = [seed]
 
     def one_step():
+        if t_ep[0] == T:  # every episode is done: a new one on the same graphs (experiments/utils.py:126-147)
+            ep_seed[0] += 1
+            env.reset(graph_ids=gids_dev, seed=ep_seed[0])
+            t_ep[0] = 0
         net.forward_graphs(env.obs_x, store, gids, norm_scope=scope[0], act=greedy, actions_out=acts)
         env.step(acts)
         scope[0] = _lib.ECO_NORM_PER_CALL_REUSE
+        t_ep[0] += 1
+
+    episode_graph = [None]
+
+    def run_steps(k):
+        """k env-steps of every episode; whole episodes from the captured graph (graphed mode)."""
+        while k > 0:
+            if graphed and episode_graph[0] is not None and k >= T and t_ep[0] in (0, T):
+                if t_ep[0] == T:
+                    ep_seed[0] += 1
+                    env.reset(graph_ids=gids_dev, seed=ep_seed[0])
+                episode_graph[0].replay()
+                t_ep[0] = T
+                k -= T
+            else:
+                one_step()
+                k -= 1
 
     for _ in range(max(args.warmup, 1)):
         one_step()
+    if graphed:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):  # captures T forward + step launches; executes nothing
+            for _ in range(T):
+                net.forward_graphs(env.obs_x, store, gids, norm_scope=_lib.ECO_NORM_PER_CALL_REUSE, act=greedy,
+                                   actions_out=acts)
+                env.step(acts)
+        episode_graph[0] = g
+        t_ep[0] = T  # the timed region starts on fresh episodes
     torch.cuda.synchronize()
     timers.clear()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -843,6 +881,12 @@ def inference_bench(args, world, rank, local, dev, dist):
     dt_rank = time.perf_counter() - t0
     dt = max_over_ranks(dt_rank, device=dev)
     pg = process_group_info(world, dt_rank, args.steps, local, dev)
+    if graphed:  # the forward launches of one eager episode, timed with HIP events on the launch stream
+        net.timer = timers
+        t_ep[0] = T
+        for _ in range(T):
+            one_step()
+        torch.cuda.synchronize()
     net.timer = None
     fwd_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in timers) / max(len(timers), 1)
     nnz = int(np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1).mean())
@@ -869,7 +913,13 @@ def inference_bench(args, world, rank, local, dev, dist):
                        "n_spins": n, "envs_per_gpu": B, "graphs": ngraphs, "max_steps": T,
                        "parallelism": f"episodes sharded, dp{world}, no collective until the best-cut reduce"},
             "roofline": dict(mfma_roofline(fl / (fwd_ms * 1e-3) / 1e12, forward_kernel_name(n, kind, ngraphs)),
-                             traffic=None, avg_launch_ms=fwd_ms, flops_per_launch=fl),
+                             traffic=None, avg_launch_ms=fwd_ms, flops_per_launch=fl,
+                             timing=("HIP events around the forward launches of one eager episode after the timed "
+                                     "region (the timed episodes replay a HIP graph)" if graphed else
+                                     "HIP events around every forward launch of the timed region")),
+            "execution": ("whole episodes (T steps: forward + fused greedy act + env step) replayed from one HIP "
+                          "graph; the episodes are reset on their graphs every T steps inside the timed region"
+                          if graphed else "eager launches"),
             "best_cut_after_steps": best_cut,
             "best_cut_note": ("random-init network after the timed steps (a throughput by-product); the full search "
                               "with the pretrained network: tools/gset_search.py, profiles/r05/gset_search_1024.json"
