@@ -436,6 +436,7 @@ def learn_loop(agent, B, world, dev, test, vector_steps=60, test_frequency=50000
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
+        regen0, reuse0 = getattr(agent, "graphs_regenerated", 0), getattr(agent, "graphs_reused", 0)
         t0 = time.perf_counter()
         agent.learn(timesteps)
         torch.cuda.synchronize()
@@ -446,6 +447,8 @@ def learn_loop(agent, B, world, dev, test, vector_steps=60, test_frequency=50000
     dt = max_over_ranks(dt_rank, device=dev)
     return {"value": agent._timestep / dt, "unit": "env-steps/s", "env_steps": agent._timestep, "seconds": dt,
             "vector_steps": vector_steps, "evaluations": n_eval, "test_frequency": test_frequency,
+            "graphs_regenerated": getattr(agent, "graphs_regenerated", 0) - regen0,
+            "graphs_reused": getattr(agent, "graphs_reused", 0) - reuse0,
             "save_network_frequency": save_network_frequency,
             "what": "DQN.learn() end to end: start() (every episode reset on fresh graphs), act + env step + replay "
                     "add + gradient steps per vector step, one evaluation per test_frequency crossing (50 test "
@@ -558,7 +561,7 @@ STAGGER_EPISODES = False  # DQN.stagger_episodes: episodes spread over the T pha
 
 
 def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1234, replay_episodes=None,
-                      n_graphs=None, regenerate=True):
+                      n_graphs=None, regenerate=True, spare_batches=0):
     """The benched configs[2] / configs[3] agent: B episodes on a pool of B seeded graphs (one per episode),
     experiments/train_eco.py:114-169 hyper-parameters (N=200: :368-377) batched, with the large-batch recipe of
     tests/test_training_quality_gpu.py (lr 1e-4 x sqrt(M / 64); target sync every TARGET_SYNC_GRAD_STEPS gradient
@@ -573,6 +576,9 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     graph_slots_needed(B, T, ring) slots (two batches of B at one episode's ring), generated on the device, and
     DQN(regenerate_graphs=) regenerates a batch's slots at each reset once no stored transition references them.
     regenerate=False: a fixed pool of n_graphs (default B) seeded graphs that episodes draw from at each reset.
+    spare_batches: extra batches of B slots for resets outside episode boundaries (the bench's untimed reset and
+    learn_loop's start() follow the timed steps mid-episode, while the replay still references the first batch),
+    so that those resets, too, draw freshly generated graphs.
     Returns (agent, store, env, lr)."""
     from eco_hip.graphs import GraphStore
     from eco_hip.envs.batched import VecSpinSystem
@@ -583,7 +589,8 @@ def build_train_agent(dev, B, n, graph="ER", gparam=0.15, minibatch=2048, seed=1
     T = 2 * n
     cap = int(B * T * (REPLAY_EPISODES if replay_episodes is None else replay_episodes))
     if regenerate:
-        store = GraphStore.generated(graph, graph_slots_needed(B, T, cap), n, gparam, seed=seed, device=dev)
+        store = GraphStore.generated(graph, graph_slots_needed(B, T, cap) + spare_batches * B, n, gparam, seed=seed,
+                                     device=dev)
     else:
         store = GraphStore.random(graph, n_graphs or B, n, gparam, seed=seed, device=dev)
     env = VecSpinSystem(store, B, T, observables=DEFAULT_OBSERVABLES, reward_signal=RewardSignal.BLS,
@@ -660,7 +667,8 @@ def main():
     T = 2 * n
     seed = 1234 + rank
     gparam = args.param if args.param is not None else (0.15 if args.graph == "ER" else 4)
-    agent, store, env, lr = build_train_agent(dev, B, n, args.graph, gparam, args.minibatch, seed)
+    agent, store, env, lr = build_train_agent(dev, B, n, args.graph, gparam, args.minibatch, seed,
+                                              spare_batches=1 if args.workload == "train" else 0)
     nnz = np.diff(store.row_ptr.cpu().numpy(), axis=1).sum(axis=1)
     gflops = np.array([mpnn_flops(z, n) for z in nnz])
     agent.start()
